@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py -- windows/s of the MI355X spectrum hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config north_star]
+
+One step = one launch of the hot path over the configuration's whole window
+batch, input already resident in HBM (series generated on device).  N > 1 is
+launched by torch.distributed.run: every rank owns a full, independent batch
+on its own GPU (weak scaling, no data-path collective; a CPU gloo group only
+brackets the timed region with barriers and takes the max time over ranks).
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus
+`roofline` (live HIP-event kernel time vs HBM peak) and `cpu_baseline` (the
+oracle -- CPU restatement of the reference path -- timed on a bounded sample
+on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "fft-wavespec_amd"))
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "FFT-windows/sec"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="north_star", choices=["c2", "c3", "north_star", "c4"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+class Control:
+    """Barrier + max-over-ranks on a CPU gloo group (no GPU collective)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed_steps(step, sync, ctl: Control, steps: int, warmup: int) -> float:
+    """W untimed steps, then K steps bracketed by barrier + device sync; returns max seconds over ranks."""
+    for _ in range(warmup):
+        step()
+    sync()
+    ctl.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    ctl.barrier()
+    t1 = time.perf_counter()
+    return ctl.max(t1 - t0)
+
+
+def cpu_baseline(series_host: np.ndarray, cfg: dict, budget_s: float) -> dict:
+    """Oracle (CPU restatement of the reference per-window path, C -O3) on
+    1 core, on leading windows of the same workload, for ~budget_s seconds."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    lib = oracle.lib()
+    lib.ora_set_threads(1)
+    n, hop = cfg["n"], cfg["hop"]
+    chunk = 64
+    done, t0 = 0, time.perf_counter()
+    max_w = 1 + (series_host.size - n) // hop
+    while time.perf_counter() - t0 < budget_s and done < max_w:
+        take = min(chunk, max_w - done)
+        seg = series_host[done * hop: (done + take - 1) * hop + n]
+        oracle.batch_spectrum(seg, n, hop, cfg["detrend"], cfg["window"], cfg.get("trend_period", 0),
+                              kalman=oracle.KALMAN_DEFAULTS)
+        done += take
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "windows/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} windows of the same {cfg['windows']}x{n} workload (hop={hop}, "
+                      f"{cfg['detrend']} detrend, {cfg['window']} window), oracle/wavespec_oracle.c -O3, "
+                      f"1 thread, {dt:.1f} s"}
+
+
+def load_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    p = ROOT / "profiles" / "traffic.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get(config, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    rank, local_rank, world = dist_env()
+    import torch
+    from wavespec_amd import bridge, synth
+
+    cfg = dict(synth.CONFIGS[args.config])
+    cfg.setdefault("trend_period", 0)
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    ctl = Control(world)
+
+    n, hop, w = cfg["n"], cfg["hop"], cfg["windows"]
+    f32 = cfg["precision"] == "f32"
+    tdt = torch.float32 if f32 else torch.float64
+    length = (w - 1) * hop + n
+    d_series = synth.random_walk_torch(length, cfg["seed"] + 1000 * rank, dev, tdt)  # resident in HBM
+    rec = n // 2
+    d_out = torch.empty(w * rec, dtype=tdt, device=dev)
+    plan = bridge.Plan(local_rank, n, hop, w, cfg["detrend"], cfg["window"], cfg["trend_period"],
+                       cfg["precision"], "power")
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step():
+        plan.execute(d_series.data_ptr(), d_out.data_ptr(), sptr)
+
+    sync = torch.cuda.synchronize
+    secs = timed_steps(step, sync, ctl, args.steps, args.warmup)
+
+    # live kernel time with HIP events on the launch stream (roofline)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = max(10, min(args.steps, 50))
+    ev0.record(stream)
+    for _ in range(reps):
+        step()
+    ev1.record(stream)
+    ev1.synchronize()
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    alg_bytes = plan.algorithmic_bytes
+    achieved = alg_bytes / kernel_s / 1e9
+
+    total_windows = ctl.sum(float(w * args.steps))
+    value = total_windows / secs
+    baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample_windows = min(w, 4096)
+        host = d_series[: (sample_windows - 1) * hop + n].double().cpu().numpy()
+        baseline = cpu_baseline(host, cfg, args.cpu_seconds)
+
+    if rank == 0:
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": secs / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if f32 else "f64",
+            "data": "synthetic (random-walk close prices generated on device, seed per rank)",
+            "config": {"workload": f"{args.config}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, "
+                                   f"{cfg['detrend']} detrend, {cfg['window']} window, |X|^2 k<N/2",
+                       "windows_per_gpu": w, "window_len": n, "hop": hop, "parallelism": f"windows sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_s * 1e3},
+            "cpu_baseline": baseline,
+        }
+        print(json.dumps(line), flush=True)
+    plan.close()
+    ctl.close()
+
+
+if __name__ == "__main__":
+    main()

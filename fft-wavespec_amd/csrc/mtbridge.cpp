@@ -1,0 +1,792 @@
+// mtbridge.cpp -- C ABI of libmtbridge.so (include/mtbridge.h): the Linux /
+// MI355X drop-in for `mt-bridge.dll` (reference Include/imports.mqh:4-20).
+//
+// Layers:
+//   * thread-local last error          (gpu_get_last_error_w, 1.1.0:742-745)
+//   * caching device / pinned-host allocator (per device, size buckets)
+//   * per-device twiddle + window tables (built once, fp64 exact on host)
+//   * enqueue(): the device hot path = [Kalman pre-pass] + spectrum kernel
+//   * Batch: H2D from pinned staging -> enqueue -> D2H, one part per GPU
+//     (windows sharded in contiguous ranges, no collective: SURVEY 8e)
+//   * session (gpu_init/gpu_shutdown), job table (submit/try_get/free),
+//     device-resident plans (wsp_plan_*).
+// Every entry point is thread-safe; the product path has no CPU fallback
+// (CHANGELOG.md:5,15 "sem fallback CPU"): without a GPU it fails with
+// MTB_BACKEND_UNAVAILABLE.
+#include "../../include/mtbridge.h"
+#include "wsp_internal.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+using namespace wsp;
+
+// ------------------------------------------------------------- last error
+thread_local std::string t_last_error;
+
+void set_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_last_error = buf;
+}
+
+#define HIP_OR(expr, code)                                                                          \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) {                                                                     \
+            set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return (code);                                                                          \
+        }                                                                                           \
+    } while (0)
+
+int device_count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// ------------------------------------------------------ caching allocator
+// Size-bucketed free lists (power-of-two buckets >= 64 KiB).  Device
+// buffers per device; pinned host buffers shared.  Keeps hipMalloc /
+// hipHostMalloc out of the per-bar path (gpu_fft_real_forward runs every
+// bar, 1.1.0:1249).
+size_t bucket_bytes(size_t n) {
+    size_t b = 64 * 1024;
+    while (b < n) b <<= 1;
+    return b;
+}
+
+struct Pool {
+    std::mutex mu;
+    std::map<std::pair<int, size_t>, std::vector<void *>> free_dev;  // (device, bytes)
+    std::map<size_t, std::vector<void *>> free_host;
+};
+Pool &pool() {
+    static Pool *p = new Pool();  // intentionally leaked: no teardown after the HIP runtime
+    return *p;
+}
+
+void *dev_alloc(int dev, size_t bytes) {
+    const size_t b = bucket_bytes(bytes);
+    {
+        std::lock_guard<std::mutex> lk(pool().mu);
+        auto &v = pool().free_dev[{dev, b}];
+        if (!v.empty()) {
+            void *p = v.back();
+            v.pop_back();
+            return p;
+        }
+    }
+    void *p = nullptr;
+    if (hipSetDevice(dev) != hipSuccess || hipMalloc(&p, b) != hipSuccess) {
+        set_error("hipMalloc(%zu bytes) failed on device %d", b, dev);
+        return nullptr;
+    }
+    return p;
+}
+void dev_free(int dev, void *p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().free_dev[{dev, bucket_bytes(bytes)}].push_back(p);
+}
+void *host_alloc(size_t bytes) {
+    const size_t b = bucket_bytes(bytes);
+    {
+        std::lock_guard<std::mutex> lk(pool().mu);
+        auto &v = pool().free_host[b];
+        if (!v.empty()) {
+            void *p = v.back();
+            v.pop_back();
+            return p;
+        }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+        set_error("hipHostMalloc(%zu bytes) failed", b);
+        return nullptr;
+    }
+    return p;
+}
+void host_free(void *p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().free_host[bucket_bytes(bytes)].push_back(p);
+}
+void pool_release_all() {
+    std::lock_guard<std::mutex> lk(pool().mu);
+    for (auto &kv : pool().free_dev) {
+        hipSetDevice(kv.first.first);
+        for (void *p : kv.second) hipFree(p);
+    }
+    pool().free_dev.clear();
+    for (auto &kv : pool().free_host)
+        for (void *p : kv.second) hipHostFree(p);
+    pool().free_host.clear();
+}
+
+// ----------------------------------------------------------------- tables
+// W_N^k = exp(-2 pi i k/N), k < N/2, rounded once from long double.
+// Window coefficients: the exact expressions of L/WaveSpecZZ_1.0.2.mq5:884-922
+// evaluated in double on the host (bit-identical to the CPU path).
+double window_value(int type, int i, int n) {
+    switch (type) {
+    case MTB_WINDOW_HANN: return 0.5 * (1.0 - cos(2.0 * M_PI * i / (n - 1)));
+    case MTB_WINDOW_HAMMING: return 0.54 - 0.46 * cos(2.0 * M_PI * i / (n - 1));
+    case MTB_WINDOW_BLACKMAN: return 0.42 - 0.5 * cos(2.0 * M_PI * i / (n - 1)) + 0.08 * cos(4.0 * M_PI * i / (n - 1));
+    case MTB_WINDOW_BARTLETT: return 1.0 - fabs((2.0 * i - n + 1) / (n - 1));
+    default: return 1.0;
+    }
+}
+
+struct Tables {
+    void *tw = nullptr;
+    void *win = nullptr;  // null = rectangular
+};
+std::mutex g_tables_mu;
+std::map<std::tuple<int, int, int, bool>, Tables> *g_tables = new std::map<std::tuple<int, int, int, bool>, Tables>();
+
+int get_tables(int dev, int log2n, int window, bool f32, Tables *out) {
+    std::lock_guard<std::mutex> lk(g_tables_mu);
+    auto key = std::make_tuple(dev, log2n, window, f32);
+    auto it = g_tables->find(key);
+    if (it != g_tables->end()) {
+        *out = it->second;
+        return MTB_OK;
+    }
+    const int n = 1 << log2n;
+    const size_t es = f32 ? sizeof(float) : sizeof(double);
+    std::vector<char> tw((size_t)n / 2 * 2 * es), win((size_t)n * es);
+    for (int k = 0; k < n / 2; ++k) {
+        const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)k / (long double)n;
+        const long double c = cosl(ang), s = sinl(ang);
+        if (f32) {
+            ((float *)tw.data())[2 * k] = (float)c;
+            ((float *)tw.data())[2 * k + 1] = (float)s;
+        } else {
+            ((double *)tw.data())[2 * k] = (double)c;
+            ((double *)tw.data())[2 * k + 1] = (double)s;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        const double wv = window_value(window, i, n);
+        if (f32) ((float *)win.data())[i] = (float)wv;
+        else ((double *)win.data())[i] = wv;
+    }
+    Tables t;
+    HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    HIP_OR(hipMalloc(&t.tw, tw.size()), MTB_NO_MEM);
+    HIP_OR(hipMemcpy(t.tw, tw.data(), tw.size(), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
+    if (window != MTB_WINDOW_NONE) {
+        HIP_OR(hipMalloc(&t.win, win.size()), MTB_NO_MEM);
+        HIP_OR(hipMemcpy(t.win, win.data(), win.size(), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
+    }
+    (*g_tables)[key] = t;
+    *out = t;
+    return MTB_OK;
+}
+
+// ----------------------------------------------------------------- config
+struct Config {
+    int n = 0, log2n = 0;
+    int64_t hop = 0, n_windows = 0;
+    int detrend = 0, window = 0, trend_period = 0, output = 0;
+    bool f32 = false;
+    size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
+    int64_t record() const { return output == MTB_OUT_PACKED ? n : n / 2; }
+    int64_t series_elems() const { return (n_windows - 1) * hop + n; }
+    int64_t unique_input_elems() const { return hop >= n ? n_windows * (int64_t)n : series_elems(); }
+};
+
+int ilog2_exact(int n) {
+    if (n <= 0 || (n & (n - 1))) return -1;
+    int l = 0;
+    while ((1 << l) < n) ++l;
+    return l;
+}
+
+int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int window, int trend_period,
+                int precision, int output, Config *c) {
+    const int l = ilog2_exact(window_len);
+    if (l < kMinLog2N || l > kMaxLog2N) {
+        set_error("window_len=%d: must be a power of two in [%d, %d]", window_len, 1 << kMinLog2N, 1 << kMaxLog2N);
+        return MTB_BAD_ARGS;
+    }
+    if (hop < 1 || n_windows < 1) {
+        set_error("hop=%lld n_windows=%lld: both must be >= 1", (long long)hop, (long long)n_windows);
+        return MTB_BAD_ARGS;
+    }
+    if (detrend < MTB_DETREND_NONE || detrend > MTB_DETREND_KALMAN || window < MTB_WINDOW_NONE ||
+        window > MTB_WINDOW_BARTLETT || (precision != MTB_PREC_F64 && precision != MTB_PREC_F32) ||
+        (output != MTB_OUT_POWER && output != MTB_OUT_PACKED)) {
+        set_error("bad mode: detrend=%d window=%d precision=%d output=%d", detrend, window, precision, output);
+        return MTB_BAD_ARGS;
+    }
+    c->n = window_len;
+    c->log2n = l;
+    c->hop = hop;
+    c->n_windows = n_windows;
+    // InpTrendPeriod <= 0 skips the trend filter (L/WaveSpecZZ_1.0.3-pla-batch.mq5:3256,3279)
+    c->detrend = (detrend == MTB_DETREND_IIR && trend_period <= 0) ? MTB_DETREND_NONE : detrend;
+    c->window = window;
+    c->trend_period = trend_period;
+    c->output = output;
+    c->f32 = precision == MTB_PREC_F32;
+    return MTB_OK;
+}
+
+// Kalman parameters (process-wide), defaults of kalman-fast.mq5:886-901.
+std::mutex g_kalman_mu;
+double g_kalman[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
+
+// ------------------------------------------------------------ device path
+// series (device) -> [Kalman pre-pass into ws] -> spectrum kernel -> out.
+int enqueue(int dev, const Config &c, const double *kalman, const void *d_series, void *d_out, void *d_ws,
+            hipStream_t s) {
+    Tables t;
+    int st = get_tables(dev, c.log2n, c.window, c.f32, &t);
+    if (st != MTB_OK) return st;
+    HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    SpectrumLaunch L{};
+    L.series = d_series;
+    L.hop = c.hop;
+    L.detrend = c.detrend;
+    if (c.detrend == MTB_DETREND_KALMAN) {
+        KalmanLaunch K{};
+        K.series = d_series;
+        K.detrended = d_ws;
+        K.hop = c.hop;
+        K.n_windows = c.n_windows;
+        K.n = c.n;
+        K.f32 = c.f32;
+        memcpy(K.params, kalman, sizeof(K.params));
+        HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
+        L.series = d_ws;
+        L.hop = c.n;
+        L.detrend = kDetrendNone;
+    }
+    L.out = d_out;
+    L.window = t.win;
+    L.twiddle = t.tw;
+    L.n_windows = c.n_windows;
+    L.log2n = c.log2n;
+    L.output = c.output;
+    L.f32 = c.f32;
+    if (L.detrend == kDetrendIir) {
+        // L/WaveSpecZZ_1.0.2.mq5:3041-3043, same double expressions as the CPU path
+        const double omega = 2.0 * M_PI / c.trend_period;
+        const double alpha = (1.0 - sin(omega)) / cos(omega);
+        L.iir_alpha = alpha;
+        L.iir_c = (1.0 - alpha) / 2.0;
+        long double p = powl((long double)alpha, 32.0L);
+        for (int j = 0; j < 8; ++j) {
+            L.iir_apow[j] = (double)p;
+            p = p * p;
+        }
+    }
+    HIP_OR(launch_spectrum(L, s), MTB_INTERNAL_ERROR);
+    return MTB_OK;
+}
+
+// ------------------------------------------------------------------ session
+struct DeviceCtx {
+    int dev = 0;
+    std::vector<hipStream_t> streams;
+    std::atomic<unsigned> rr{0};
+    hipStream_t next_stream() { return streams[rr.fetch_add(1) % streams.size()]; }
+};
+struct Session {
+    int device_index = 0;
+    std::vector<std::unique_ptr<DeviceCtx>> devs;
+};
+std::mutex g_session_mu;
+std::shared_ptr<Session> g_session;
+
+std::shared_ptr<Session> session() {
+    std::lock_guard<std::mutex> lk(g_session_mu);
+    return g_session;
+}
+
+// -------------------------------------------------------------------- batch
+// One request split over the session's devices; owns pinned staging and
+// device buffers until released.  Used synchronously and as an async job.
+struct Part {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    int64_t w0 = 0, nw = 0;
+    void *d_in = nullptr, *d_out = nullptr, *d_ws = nullptr;
+    size_t in_bytes = 0, out_bytes = 0, ws_bytes = 0;
+};
+struct Batch {
+    Config cfg;
+    double kalman[16];
+    std::vector<Part> parts;
+    void *h_in = nullptr, *h_out = nullptr;
+    size_t h_in_bytes = 0, h_out_bytes = 0;
+    int status = MTB_OK;
+    std::string error;
+    ~Batch() {
+        for (auto &p : parts) {
+            if (p.done) {
+                hipSetDevice(p.dev);
+                hipEventSynchronize(p.done);
+                hipEventDestroy(p.done);
+            }
+            dev_free(p.dev, p.d_in, p.in_bytes);
+            dev_free(p.dev, p.d_out, p.out_bytes);
+            dev_free(p.dev, p.d_ws, p.ws_bytes);
+        }
+        host_free(h_in, h_in_bytes);
+        host_free(h_out, h_out_bytes);
+    }
+};
+
+// Stages `series` (double, chronological) and enqueues every part.
+int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out) {
+    auto b = std::make_unique<Batch>();
+    b->cfg = c;
+    {
+        std::lock_guard<std::mutex> lk(g_kalman_mu);
+        memcpy(b->kalman, g_kalman, sizeof(g_kalman));
+    }
+    const size_t es = c.elem();
+    const int64_t in_elems = c.series_elems();
+    b->h_in_bytes = (size_t)in_elems * es;
+    b->h_out_bytes = (size_t)(c.n_windows * c.record()) * es;
+    b->h_in = host_alloc(b->h_in_bytes);
+    b->h_out = host_alloc(b->h_out_bytes);
+    if (!b->h_in || !b->h_out) return MTB_NO_MEM;
+    if (c.f32) {
+        float *dst = (float *)b->h_in;
+        for (int64_t i = 0; i < in_elems; ++i) dst[i] = (float)series[i];
+    } else {
+        memcpy(b->h_in, series, b->h_in_bytes);
+    }
+    const int G = (int)std::min<int64_t>((int64_t)S.devs.size(), c.n_windows);
+    const int64_t per = (c.n_windows + G - 1) / G;
+    for (int g = 0; g < G; ++g) {
+        Part p;
+        DeviceCtx &D = *S.devs[g];
+        p.dev = D.dev;
+        p.w0 = g * per;
+        p.nw = std::min<int64_t>(per, c.n_windows - p.w0);
+        if (p.nw <= 0) break;
+        Config pc = c;
+        pc.n_windows = p.nw;
+        p.in_bytes = (size_t)pc.series_elems() * es;
+        p.out_bytes = (size_t)(p.nw * c.record()) * es;
+        p.ws_bytes = c.detrend == MTB_DETREND_KALMAN ? (size_t)(p.nw * c.n) * es : 0;
+        p.stream = D.next_stream();
+        b->parts.push_back(p);
+        Part &P = b->parts.back();
+        HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
+        P.d_in = dev_alloc(P.dev, P.in_bytes);
+        P.d_out = dev_alloc(P.dev, P.out_bytes);
+        if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
+        if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
+        HIP_OR(hipEventCreateWithFlags(&P.done, hipEventDisableTiming), MTB_INTERNAL_ERROR);
+        const char *src = (const char *)b->h_in + (size_t)(P.w0 * c.hop) * es;
+        HIP_OR(hipMemcpyAsync(P.d_in, src, P.in_bytes, hipMemcpyHostToDevice, P.stream), MTB_INTERNAL_ERROR);
+        int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
+        if (st != MTB_OK) return st;
+        char *dst = (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
+        HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
+        HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+    }
+    *out = std::move(b);
+    return MTB_OK;
+}
+
+// MTB_OK when every part finished, MTB_NOT_READY otherwise (non-blocking
+// unless `wait`).
+int batch_poll(Batch &b, bool wait) {
+    for (auto &p : b.parts) {
+        hipSetDevice(p.dev);
+        hipError_t e = wait ? hipEventSynchronize(p.done) : hipEventQuery(p.done);
+        if (e == hipErrorNotReady) return MTB_NOT_READY;
+        if (e != hipSuccess) {
+            set_error("device %d: %s", p.dev, hipGetErrorString(e));
+            return MTB_INTERNAL_ERROR;
+        }
+    }
+    return MTB_OK;
+}
+
+// Copies finished records (converted to double) into the caller's buffer.
+int32_t batch_copy_out(const Batch &b, double *out, int64_t out_cap) {
+    const int64_t rec = b.cfg.record();
+    const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
+    const int64_t n = nrec * rec;
+    if (b.cfg.f32) {
+        const float *src = (const float *)b.h_out;
+        for (int64_t i = 0; i < n; ++i) out[i] = (double)src[i];
+    } else {
+        memcpy(out, b.h_out, (size_t)n * sizeof(double));
+    }
+    return (int32_t)nrec;
+}
+
+int run_sync(const Config &c, const double *series, double *out, int64_t out_cap, int32_t *out_len) {
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    std::unique_ptr<Batch> b;
+    int st = batch_start(*S, c, series, &b);
+    if (st != MTB_OK) return st;
+    st = batch_poll(*b, true);
+    if (st != MTB_OK) return st;
+    const int32_t n = batch_copy_out(*b, out, out_cap);
+    if (out_len) *out_len = n;
+    return MTB_OK;
+}
+
+// --------------------------------------------------------------------- jobs
+std::mutex g_jobs_mu;
+std::map<int64_t, std::unique_ptr<Batch>> *g_jobs = new std::map<int64_t, std::unique_ptr<Batch>>();
+std::atomic<int64_t> g_next_id{1};
+
+// -------------------------------------------------------------------- plans
+struct Plan {
+    int dev = 0;
+    Config cfg;
+    double kalman[16];
+    void *d_ws = nullptr;
+    size_t ws_bytes = 0;
+};
+std::mutex g_plans_mu;
+std::map<int64_t, std::unique_ptr<Plan>> *g_plans = new std::map<int64_t, std::unique_ptr<Plan>>();
+
+}  // namespace
+
+// =========================================================================
+extern "C" {
+
+MTB_API const char *wsp_version(void) { return "mtbridge-mi355x 0.1.0 gfx950"; }
+
+MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count) {
+    std::lock_guard<std::mutex> lk(g_session_mu);
+    if (g_session && g_session->device_index == device_index) return MTB_OK;
+    const int n = device_count();
+    if (n <= 0) {
+        set_error("no HIP device visible (hipGetDeviceCount=0); the spectrum path has no CPU fallback");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    if (device_index < -1 || device_index >= n) {
+        set_error("device_index=%d out of range (%d devices, -1 = all)", device_index, n);
+        return MTB_BAD_ARGS;
+    }
+    const int streams = std::max(1, std::min(512, (int)stream_count));
+    auto S = std::make_shared<Session>();
+    S->device_index = device_index;
+    const int first = device_index < 0 ? 0 : device_index;
+    const int last = device_index < 0 ? n - 1 : device_index;
+    for (int d = first; d <= last; ++d) {
+        auto D = std::make_unique<DeviceCtx>();
+        D->dev = d;
+        HIP_OR(hipSetDevice(d), MTB_BACKEND_UNAVAILABLE);
+        for (int s = 0; s < streams; ++s) {
+            hipStream_t st;
+            HIP_OR(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), MTB_BACKEND_UNAVAILABLE);
+            D->streams.push_back(st);
+        }
+        S->devs.push_back(std::move(D));
+    }
+    g_session = S;
+    return MTB_OK;
+}
+
+MTB_API void gpu_shutdown(void) {
+    {
+        std::lock_guard<std::mutex> lk(g_jobs_mu);
+        g_jobs->clear();  // ~Batch waits for in-flight work
+    }
+    std::shared_ptr<Session> S;
+    {
+        std::lock_guard<std::mutex> lk(g_session_mu);
+        S = std::move(g_session);
+        g_session.reset();
+    }
+    if (S) {
+        for (auto &D : S->devs) {
+            hipSetDevice(D->dev);
+            for (auto st : D->streams) {
+                hipStreamSynchronize(st);
+                hipStreamDestroy(st);
+            }
+        }
+    }
+    pool_release_all();
+}
+
+MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out) {
+    if (!in || !out) {
+        set_error("gpu_fft_real_forward: null buffer");
+        return MTB_BAD_ARGS;
+    }
+    Config c;
+    int st = make_config(len, len, 1, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64, MTB_OUT_PACKED, &c);
+    if (st != MTB_OK) return st;
+    int32_t n = 0;
+    return run_sync(c, in, out, len, &n);
+}
+
+MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len, int32_t n_windows, double *out) {
+    if (!in || !out) {
+        set_error("gpu_fft_real_forward_batch: null buffer");
+        return MTB_BAD_ARGS;
+    }
+    Config c;
+    int st = make_config(window_len, window_len, n_windows, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64,
+                         MTB_OUT_PACKED, &c);
+    if (st != MTB_OK) return st;
+    int32_t n = 0;
+    return run_sync(c, in, out, (int64_t)window_len * n_windows, &n);
+}
+
+static int spectrum_config(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
+                           int32_t detrend, int32_t window, int32_t trend_period, int32_t precision, int32_t output,
+                           Config *c) {
+    if (!series) {
+        set_error("null series");
+        return MTB_BAD_ARGS;
+    }
+    if (window_len <= 0 || series_len < window_len || hop <= 0) {
+        set_error("series_len=%d window_len=%d hop=%d: need series_len >= window_len > 0, hop > 0", series_len,
+                  window_len, hop);
+        return MTB_BAD_ARGS;
+    }
+    const int64_t nwin = 1 + ((int64_t)series_len - window_len) / hop;  // 1.1.0:1016
+    return make_config(window_len, hop, nwin, detrend, window, trend_period, precision, output, c);
+}
+
+MTB_API int32_t gpu_spectrum_batch(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
+                                   int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
+                                   int32_t output, double *out, int32_t out_cap, int32_t *out_len) {
+    if (out_len) *out_len = 0;
+    Config c;
+    int st = spectrum_config(series, series_len, window_len, hop, detrend, window, trend_period, precision, output, &c);
+    if (st != MTB_OK) return st;
+    if (!out || out_cap < c.record()) {
+        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)c.record());
+        return MTB_BAD_ARGS;
+    }
+    // only the records that fit are computed
+    c.n_windows = std::min<int64_t>(c.n_windows, out_cap / c.record());
+    return run_sync(c, series, out, out_cap, out_len);
+}
+
+MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_len, int32_t window_len,
+                                          int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
+                                          int32_t precision, int32_t output, int64_t *job_id) {
+    if (!job_id) {
+        set_error("null job_id");
+        return MTB_BAD_ARGS;
+    }
+    *job_id = 0;
+    Config c;
+    int st = spectrum_config(series, series_len, window_len, hop, detrend, window, trend_period, precision, output, &c);
+    if (st != MTB_OK) return st;
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    std::unique_ptr<Batch> b;
+    st = batch_start(*S, c, series, &b);
+    if (st != MTB_OK) return st;
+    const int64_t id = g_next_id.fetch_add(1);
+    {
+        std::lock_guard<std::mutex> lk(g_jobs_mu);
+        (*g_jobs)[id] = std::move(b);
+    }
+    *job_id = id;
+    return MTB_OK;
+}
+
+MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t out_cap, int32_t *out_len,
+                                           int32_t *ready) {
+    if (ready) *ready = 0;
+    if (out_len) *out_len = 0;
+    std::lock_guard<std::mutex> lk(g_jobs_mu);
+    auto it = g_jobs->find(job_id);
+    if (it == g_jobs->end()) {
+        set_error("unknown job id %lld", (long long)job_id);
+        return MTB_BAD_ARGS;
+    }
+    Batch &b = *it->second;
+    const int st = batch_poll(b, false);
+    if (st == MTB_NOT_READY) return MTB_NOT_READY;
+    if (ready) *ready = 1;
+    if (st != MTB_OK) return st;
+    if (!out || out_cap < b.cfg.record()) {
+        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)b.cfg.record());
+        return MTB_BAD_ARGS;
+    }
+    const int32_t n = batch_copy_out(b, out, out_cap);
+    if (out_len) *out_len = n;
+    return MTB_OK;
+}
+
+MTB_API int32_t gpu_free_job(int64_t job_id) {
+    std::unique_ptr<Batch> b;
+    {
+        std::lock_guard<std::mutex> lk(g_jobs_mu);
+        auto it = g_jobs->find(job_id);
+        if (it == g_jobs->end()) {
+            set_error("unknown job id %lld", (long long)job_id);
+            return MTB_BAD_ARGS;
+        }
+        b = std::move(it->second);
+        g_jobs->erase(it);
+    }
+    return MTB_OK;  // ~Batch waits for the device and recycles buffers
+}
+
+MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n) {
+    if (!params || n != 16) {
+        set_error("gpu_set_kalman_params: need 16 parameters, got %d", n);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(g_kalman_mu);
+    memcpy(g_kalman, params, sizeof(g_kalman));
+    return MTB_OK;
+}
+
+// ---- cycle extraction: not part of the spectrum hot path -----------------
+#define CYCLES_UNAVAILABLE(name)                                                                         \
+    set_error(name ": MUSIC/ESPRIT cycle extraction is outside the MI355X spectrum path (SURVEY 2 row 13)"); \
+    return MTB_BACKEND_UNAVAILABLE
+
+MTB_API int32_t gpu_extract_cycles(const double *, int32_t, int32_t, double, double, double, int32_t, int32_t,
+                                   double *, int32_t, int32_t, int32_t *out_len) {
+    if (out_len) *out_len = 0;
+    CYCLES_UNAVAILABLE("gpu_extract_cycles");
+}
+MTB_API int32_t gpu_submit_extract_cycles(const double *, int32_t, int32_t, double, double, double, int32_t, int32_t,
+                                          int64_t *job_id) {
+    if (job_id) *job_id = 0;
+    CYCLES_UNAVAILABLE("gpu_submit_extract_cycles");
+}
+MTB_API int32_t gpu_try_get_cycles(int64_t, double *, int32_t, int32_t, int32_t *out_len, int32_t *ready) {
+    if (out_len) *out_len = 0;
+    if (ready) *ready = 0;
+    CYCLES_UNAVAILABLE("gpu_try_get_cycles");
+}
+MTB_API int32_t gpu_submit_extract_cycles_batch(const double *, int32_t, int32_t, int32_t, int32_t, double, double,
+                                                double, int32_t, int32_t, int32_t, int64_t *job_id) {
+    if (job_id) *job_id = 0;
+    CYCLES_UNAVAILABLE("gpu_submit_extract_cycles_batch");
+}
+MTB_API int32_t gpu_try_get_cycles_batch(int64_t, double *, int32_t, int32_t *out_len, int32_t *ready) {
+    if (out_len) *out_len = 0;
+    if (ready) *ready = 0;
+    CYCLES_UNAVAILABLE("gpu_try_get_cycles_batch");
+}
+
+MTB_API int32_t gpu_get_last_error_w(uint16_t *buf, int32_t buf_len) {
+    const std::string &e = t_last_error;
+    if (!buf || buf_len <= 0 || e.empty()) return 0;
+    const int32_t n = (int32_t)std::min<size_t>(e.size(), (size_t)buf_len - 1);
+    for (int32_t i = 0; i < n; ++i) buf[i] = (uint16_t)(unsigned char)e[i];
+    buf[n] = 0;
+    return n + 1;
+}
+
+// ---- device-resident plans -------------------------------------------------
+MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop, int64_t n_windows, int32_t detrend,
+                                int32_t window, int32_t trend_period, int32_t precision, int32_t output) {
+    const int n = device_count();
+    if (n <= 0) {
+        set_error("no HIP device visible; the spectrum path has no CPU fallback");
+        return 0;
+    }
+    if (device < 0 || device >= n) {
+        set_error("device %d out of range (%d devices)", device, n);
+        return 0;
+    }
+    auto p = std::make_unique<Plan>();
+    if (make_config(window_len, hop, n_windows, detrend, window, trend_period, precision, output, &p->cfg) != MTB_OK)
+        return 0;
+    p->dev = device;
+    {
+        std::lock_guard<std::mutex> lk(g_kalman_mu);
+        memcpy(p->kalman, g_kalman, sizeof(g_kalman));
+    }
+    Tables t;
+    if (get_tables(device, p->cfg.log2n, p->cfg.window, p->cfg.f32, &t) != MTB_OK) return 0;
+    if (p->cfg.detrend == MTB_DETREND_KALMAN) {
+        p->ws_bytes = (size_t)(p->cfg.n_windows * p->cfg.n) * p->cfg.elem();
+        if (hipSetDevice(device) != hipSuccess || hipMalloc(&p->d_ws, p->ws_bytes) != hipSuccess) {
+            set_error("hipMalloc(%zu) for the Kalman workspace failed", p->ws_bytes);
+            return 0;
+        }
+    }
+    const int64_t id = g_next_id.fetch_add(1);
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    (*g_plans)[id] = std::move(p);
+    return id;
+}
+
+MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream) {
+    Plan *p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_plans_mu);
+        auto it = g_plans->find(plan);
+        if (it != g_plans->end()) p = it->second.get();
+    }
+    if (!p) {
+        set_error("unknown plan %lld", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    if (!d_series || !d_out) {
+        set_error("wsp_plan_execute: null device buffer");
+        return MTB_BAD_ARGS;
+    }
+    return enqueue(p->dev, p->cfg, p->kalman, d_series, d_out, p->d_ws, (hipStream_t)hip_stream);
+}
+
+MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan) {
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    auto it = g_plans->find(plan);
+    if (it == g_plans->end()) return -1;
+    const Config &c = it->second->cfg;
+    return (c.unique_input_elems() + c.n_windows * c.record()) * (int64_t)c.elem();
+}
+
+MTB_API int32_t wsp_plan_destroy(int64_t plan) {
+    std::unique_ptr<Plan> p;
+    {
+        std::lock_guard<std::mutex> lk(g_plans_mu);
+        auto it = g_plans->find(plan);
+        if (it == g_plans->end()) {
+            set_error("unknown plan %lld", (long long)plan);
+            return MTB_BAD_ARGS;
+        }
+        p = std::move(it->second);
+        g_plans->erase(it);
+    }
+    if (p->d_ws) {
+        hipSetDevice(p->dev);
+        hipDeviceSynchronize();
+        hipFree(p->d_ws);
+    }
+    return MTB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// wsp_internal.h -- internal interface between the C-ABI layer (mtbridge.cpp)
+// and the gfx950 kernels (spectrum_kernels.hip, kalman_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wsp {
+
+// Smallest / largest window the single-workgroup kernel handles.  N = 2M,
+// M complex points per window live in one workgroup's LDS (SURVEY.md sec. 5
+// "Long-context analogue": N <= 4096 fp64 fits one workgroup).
+constexpr int kMinLog2N = 5;   // N = 32
+constexpr int kMaxLog2N = 12;  // N = 4096
+constexpr int kBlock = 128;    // threads per workgroup (2 waves)
+
+enum Detrend : int { kDetrendNone = 0, kDetrendMean = 1, kDetrendIir = 2, kDetrendKalman = 3 };
+enum Output : int { kOutPower = 0, kOutPacked = 1 };
+
+// Everything a spectrum launch needs; pointer types are erased so one
+// struct serves the f64 and f32 instantiations.
+struct SpectrumLaunch {
+    const void *series;   // window w starts at series + w*hop (elements)
+    void *out;            // n_windows records of N/2 (power) or N (packed)
+    const void *window;   // N window coefficients (element type), or null = rectangular
+    const void *twiddle;  // N/2 complex W_N^k, element type
+    int64_t hop;
+    int64_t n_windows;
+    int log2n;
+    int detrend;          // kDetrendNone/Mean/Iir (Kalman runs as a pre-pass)
+    int output;
+    bool f32;
+    // IIR trend coefficients (L/WaveSpecZZ_1.0.2.mq5:3041-3043), always fp64
+    double iir_alpha, iir_c;
+    double iir_apow[8];   // alpha^(32 * 2^j), j = 0..7
+    int grid;             // 0 = auto
+};
+
+hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);
+
+// Per-window Kalman 4D detrend pre-pass: d[w*N + j] = x_j - trend_j
+// (one lane per window; trend arithmetic in fp64 like the MQL5 source).
+struct KalmanLaunch {
+    const void *series;
+    void *detrended;      // n_windows * N elements, element type of the plan
+    int64_t hop;
+    int64_t n_windows;
+    int n;
+    bool f32;
+    double params[16];    // L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901 order
+};
+
+hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream);
+
+}  // namespace wsp

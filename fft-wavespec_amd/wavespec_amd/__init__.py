@@ -1,0 +1,8 @@
+"""wavespec_amd -- MI355X-native spectrum hot path of WaveSpecZZ.
+
+The product is libmtbridge.so (HIP for gfx950, C ABI of include/mtbridge.h);
+this package is its Python host mirror.  See DESIGN.md.
+"""
+from . import bridge, indicator, synth  # noqa: F401
+
+__all__ = ["bridge", "indicator", "synth"]

@@ -1,0 +1,205 @@
+"""ctypes binding of libmtbridge.so (include/mtbridge.h).
+
+This is the Python view of the C ABI that replaces ``mt-bridge.dll``
+(reference ``Include/imports.mqh:4-20``).  It adds nothing to the compute
+path: every call goes straight into the HIP library.  If the library is
+missing the import of :func:`lib` raises -- there is no CPU fallback
+(reference ``CHANGELOG.md:5,15``: "sem fallback CPU").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent  # fft-wavespec_amd/
+LIB_PATH = PKG_ROOT / "lib" / "libmtbridge.so"
+
+# status codes (L/WaveSpecZZ_gpu_wip.mq5:263-269)
+OK, BAD_ARGS, BACKEND_UNAVAILABLE, TIMEOUT, INTERNAL_ERROR, NOT_READY, NO_MEM = 0, -1, -2, -3, -4, -5, -6
+STATUS_NAMES = {OK: "OK", BAD_ARGS: "BAD_ARGS", BACKEND_UNAVAILABLE: "BACKEND_UNAVAILABLE", TIMEOUT: "TIMEOUT",
+                INTERNAL_ERROR: "INTERNAL", NOT_READY: "NOT_READY", NO_MEM: "NO_MEM"}
+DETREND = {"none": 0, "mean": 1, "iir": 2, "kalman": 3}
+WINDOW = {"none": 0, "hann": 1, "hamming": 2, "blackman": 3, "bartlett": 4}
+PRECISION = {"f64": 0, "f32": 1}
+OUTPUT = {"power": 0, "packed": 1}
+
+_d = C.POINTER(C.c_double)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); exactly the prototypes of include/mtbridge.h
+SIGNATURES = {
+    "gpu_init": (C.c_int32, [C.c_int32, C.c_int32]),
+    "gpu_shutdown": (None, []),
+    "gpu_fft_real_forward": (C.c_int32, [_d, C.c_int32, _d]),
+    "gpu_extract_cycles": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_double, C.c_int32,
+                                       C.c_int32, _d, C.c_int32, C.c_int32, _i32p]),
+    "gpu_submit_extract_cycles": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_double,
+                                              C.c_int32, C.c_int32, _i64p]),
+    "gpu_try_get_cycles": (C.c_int32, [C.c_int64, _d, C.c_int32, C.c_int32, _i32p, _i32p]),
+    "gpu_submit_extract_cycles_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,
+                                                    C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32, _i64p]),
+    "gpu_try_get_cycles_batch": (C.c_int32, [C.c_int64, _d, C.c_int32, _i32p, _i32p]),
+    "gpu_free_job": (C.c_int32, [C.c_int64]),
+    "gpu_get_last_error_w": (C.c_int32, [C.POINTER(C.c_uint16), C.c_int32]),
+    "gpu_fft_real_forward_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, _d]),
+    "gpu_spectrum_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_int32, C.c_int32, _d, C.c_int32, _i32p]),
+    "gpu_submit_spectrum_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                              C.c_int32, C.c_int32, C.c_int32, _i64p]),
+    "gpu_try_get_spectrum_batch": (C.c_int32, [C.c_int64, _d, C.c_int32, _i32p, _i32p]),
+    "gpu_set_kalman_params": (C.c_int32, [_d, C.c_int32]),
+    "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                    C.c_int32, C.c_int32]),
+    "wsp_plan_execute": (C.c_int32, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "wsp_plan_algorithmic_bytes": (C.c_int64, [C.c_int64]),
+    "wsp_plan_destroy": (C.c_int32, [C.c_int64]),
+    "wsp_version": (C.c_char_p, []),
+}
+
+_LIB = None
+
+
+class BridgeError(RuntimeError):
+    def __init__(self, fn: str, status: int, reason: str):
+        super().__init__(f"{fn} -> {STATUS_NAMES.get(status, status)}: {reason}")
+        self.status = status
+        self.reason = reason
+
+
+def lib() -> C.CDLL:
+    """Load libmtbridge.so (fails loudly when it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        path = Path(os.environ.get("WSP_MTBRIDGE_LIB", LIB_PATH))
+        if not path.exists():
+            raise FileNotFoundError(f"{path} not built: run __graft_entry__.build() or `make -C fft-wavespec_amd`")
+        h = C.CDLL(str(path))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = h
+    return _LIB
+
+
+def last_error() -> str:
+    """gpu_get_last_error_w as MQL reads it: ShortArrayToString(buf, 0, n-1)."""
+    buf = (C.c_uint16 * 256)()
+    n = lib().gpu_get_last_error_w(buf, 256)
+    return "".join(chr(buf[i]) for i in range(n - 1)) if n > 0 else "n/a"
+
+
+def _check(fn: str, st: int) -> int:
+    if st != OK:
+        raise BridgeError(fn, st, last_error())
+    return st
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_d)
+
+
+def init(device_index: int = 0, stream_count: int = 64) -> None:
+    _check("gpu_init", lib().gpu_init(device_index, stream_count))
+
+
+def shutdown() -> None:
+    lib().gpu_shutdown()
+
+
+def fft_real_forward(x: np.ndarray) -> np.ndarray:
+    """gpu_fft_real_forward: packed out[2k]=Re X_k, out[2k+1]=Im X_k, k < N/2."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    _check("gpu_fft_real_forward", lib().gpu_fft_real_forward(_dptr(x), x.size, _dptr(out)))
+    return out
+
+
+def fft_real_forward_batch(windows: np.ndarray) -> np.ndarray:
+    w = np.ascontiguousarray(windows, dtype=np.float64)
+    out = np.empty_like(w)
+    _check("gpu_fft_real_forward_batch",
+           lib().gpu_fft_real_forward_batch(_dptr(w), w.shape[1], w.shape[0], _dptr(out)))
+    return out
+
+
+def spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
+                   trend_period: int = 0, precision="f64", output="power", max_records: int | None = None
+                   ) -> np.ndarray:
+    """gpu_spectrum_batch over a chronological series -> (nwin, record) array."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - window_len) // hop
+    rec = window_len if OUTPUT[output] == 1 else window_len // 2
+    if max_records is not None:
+        nwin = min(nwin, max_records)
+    out = np.empty((nwin, rec), dtype=np.float64)
+    n_out = C.c_int32(0)
+    _check("gpu_spectrum_batch",
+           lib().gpu_spectrum_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
+                                    trend_period, PRECISION[precision], OUTPUT[output], _dptr(out), out.size,
+                                    C.byref(n_out)))
+    return out[: n_out.value]
+
+
+def submit_spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
+                          trend_period: int = 0, precision="f64", output="power") -> int:
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    jid = C.c_int64(0)
+    _check("gpu_submit_spectrum_batch",
+           lib().gpu_submit_spectrum_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
+                                           trend_period, PRECISION[precision], OUTPUT[output], C.byref(jid)))
+    return jid.value
+
+
+def try_get_spectrum_batch(job_id: int, out: np.ndarray):
+    """Returns (status, ready, out_len) exactly as the ABI reports them."""
+    n = C.c_int32(0)
+    ready = C.c_int32(0)
+    st = lib().gpu_try_get_spectrum_batch(job_id, _dptr(out), out.size, C.byref(n), C.byref(ready))
+    return st, ready.value, n.value
+
+
+def free_job(job_id: int) -> int:
+    return lib().gpu_free_job(job_id)
+
+
+def set_kalman_params(params) -> None:
+    p = np.ascontiguousarray(params, dtype=np.float64)
+    _check("gpu_set_kalman_params", lib().gpu_set_kalman_params(_dptr(p), p.size))
+
+
+class Plan:
+    """Device-resident plan (wsp_plan_*): the hot path on buffers already in HBM."""
+
+    def __init__(self, device: int, window_len: int, hop: int, n_windows: int, detrend="none", window="hann",
+                 trend_period: int = 0, precision="f64", output="power"):
+        self.handle = lib().wsp_plan_create(device, window_len, hop, n_windows, DETREND[detrend], WINDOW[window],
+                                            trend_period, PRECISION[precision], OUTPUT[output])
+        if self.handle == 0:
+            raise BridgeError("wsp_plan_create", INTERNAL_ERROR, last_error())
+        self.window_len, self.hop, self.n_windows = window_len, hop, n_windows
+        self.record = window_len if OUTPUT[output] == 1 else window_len // 2
+        self.series_len = (n_windows - 1) * hop + window_len
+
+    @property
+    def algorithmic_bytes(self) -> int:
+        return int(lib().wsp_plan_algorithmic_bytes(self.handle))
+
+    def execute(self, d_series: int, d_out: int, stream: int = 0) -> None:
+        _check("wsp_plan_execute", lib().wsp_plan_execute(self.handle, C.c_void_p(d_series), C.c_void_p(d_out),
+                                                          C.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self.handle:
+            lib().wsp_plan_destroy(self.handle)
+            self.handle = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

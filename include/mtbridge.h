@@ -1,0 +1,186 @@
+/*
+ * mtbridge.h -- C ABI of libmtbridge.so, the MI355X-native drop-in for the
+ * `mt-bridge.dll` that WaveSpecZZ binds with `#import "mt-bridge.dll"`
+ * (reference Include/imports.mqh:4-20).
+ *
+ * Type mapping (MQL5 -> C):
+ *   int -> int32_t, long -> int64_t (NOT C long), double&[] -> double*,
+ *   int& -> int32_t*, long& -> int64_t*, ushort&[] -> uint16_t* (UTF-16).
+ * Arrays are passed as raw pointers with explicit sizes.  All buffers are
+ * caller-owned; the library never keeps a caller pointer past return.
+ * Every entry point is thread-safe (MT5 runs different charts on different
+ * threads of one process).
+ *
+ * Status codes follow L/WaveSpecZZ_gpu_wip.mq5:263-269 and
+ * WaveCyclesBatchFetcher.mq5:14-22.
+ */
+#ifndef MTBRIDGE_H
+#define MTBRIDGE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTB_API __attribute__((visibility("default")))
+
+/* ---- status codes (ALGLIB_STATUS_*) ---------------------------------- */
+#define MTB_OK 0
+#define MTB_BAD_ARGS (-1)
+#define MTB_BACKEND_UNAVAILABLE (-2)
+#define MTB_TIMEOUT (-3)
+#define MTB_INTERNAL_ERROR (-4)
+#define MTB_NOT_READY (-5)
+#define MTB_NO_MEM (-6)
+
+/* ---- enums of the spectrum batch API -------------------------------- */
+/* detrend: none (1.1.0:1239), mean (L/WaveSpecZZ_gpu_wip.mq5:940-950),
+ * IIR trend (L/WaveSpecZZ_1.0.2.mq5:3040-3053), per-window Kalman 4D
+ * (L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:2015-2125, reset per window). */
+#define MTB_DETREND_NONE 0
+#define MTB_DETREND_MEAN 1
+#define MTB_DETREND_IIR 2
+#define MTB_DETREND_KALMAN 3
+/* window: enum WINDOW_TYPE, L/WaveSpecZZ_1.0.2.mq5:626-632 */
+#define MTB_WINDOW_NONE 0
+#define MTB_WINDOW_HANN 1
+#define MTB_WINDOW_HAMMING 2
+#define MTB_WINDOW_BLACKMAN 3
+#define MTB_WINDOW_BARTLETT 4
+/* arithmetic precision of the device path */
+#define MTB_PREC_F64 0
+#define MTB_PREC_F32 1
+/* output: |X_k|^2 for k < N/2 (FftProcessor::Run 1.1.0:529-530), or the
+ * packed gpu_fft_real_forward layout out[2k]=Re X_k, out[2k+1]=Im X_k
+ * (1.1.0:522-528). */
+#define MTB_OUT_POWER 0
+#define MTB_OUT_PACKED 1
+
+/* =====================================================================
+ * 1. Reference surface -- Include/imports.mqh:5-19 (exact signatures)
+ * ===================================================================== */
+
+/* imports.mqh:5.  Opens a session on `device_index` (0-based HIP device;
+ * -1 = every visible GPU, windows of batch calls are sharded across them).
+ * `stream_count` HIP streams per device (caller clamps 16..512, 1.1.0:729).
+ * Idempotent; the caller retries it every bar until it succeeds
+ * (1.1.0:722-751).  Returns MTB_OK or MTB_BACKEND_UNAVAILABLE. */
+MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count);
+
+/* imports.mqh:6.  Frees every job, stream and buffer (OnDeinit 1.1.0:706-716). */
+MTB_API void gpu_shutdown(void);
+
+/* imports.mqh:7; caller FftProcessor::Run 1.1.0:518-531.  Real forward DFT
+ * (unnormalised, e^{-2 pi i k n/N}) of in[0..len) into out[0..len):
+ * out[2k] = Re X_k, out[2k+1] = Im X_k for k < len/2.  len: power of two,
+ * 16..4096.  Synchronous. */
+MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out);
+
+/* imports.mqh:8-19: MUSIC/ESPRIT cycle extraction lives outside the
+ * spectrum hot path.  These return
+ * MTB_BACKEND_UNAVAILABLE and set the last error. */
+MTB_API int32_t gpu_extract_cycles(const double *series, int32_t len, int32_t top_k, double min_period,
+                                   double max_period, double sample_rate_seconds, int32_t method,
+                                   int32_t ar_order, double *out, int32_t out_stride, int32_t out_capacity,
+                                   int32_t *out_len);
+MTB_API int32_t gpu_submit_extract_cycles(const double *series, int32_t len, int32_t top_k, double min_period,
+                                          double max_period, double sample_rate_seconds, int32_t method,
+                                          int32_t ar_order, int64_t *job_id);
+MTB_API int32_t gpu_try_get_cycles(int64_t job_id, double *out, int32_t out_stride, int32_t out_capacity,
+                                   int32_t *out_len, int32_t *ready);
+MTB_API int32_t gpu_submit_extract_cycles_batch(const double *series, int32_t series_len, int32_t window_len,
+                                                int32_t hop, int32_t top_k, double min_period, double max_period,
+                                                double sample_rate_seconds, int32_t method, int32_t ar_order,
+                                                int32_t stride, int64_t *job_id);
+MTB_API int32_t gpu_try_get_cycles_batch(int64_t job_id, double *out, int32_t out_cap, int32_t *out_len,
+                                         int32_t *ready);
+
+/* imports.mqh:18.  Releases a job of any kind (callers always free after a
+ * result or an error: 1.1.0:1040, 1277). Unknown id -> MTB_BAD_ARGS. */
+MTB_API int32_t gpu_free_job(int64_t job_id);
+
+/* imports.mqh:19.  Copies the calling thread's last error as UTF-16 into
+ * buf (at most buf_len units, NUL-terminated) and returns the number of
+ * units written INCLUDING the terminator (caller: ShortArrayToString(buf,
+ * 0, n-1), 1.1.0:742-744).  0 when there is no error text. */
+MTB_API int32_t gpu_get_last_error_w(uint16_t *buf, int32_t buf_len);
+
+/* =====================================================================
+ * 2. Batch FFT declared by the legacy indicators
+ *    (L/WaveSpecZZ_1.0.3-pla-batch.mq5:29, L/WaveSpecZZ_gpu_cycles.mq5:14)
+ * ===================================================================== */
+
+/* n_windows pre-materialised windows in[w*window_len + j] -> packed spectra
+ * out[w*window_len + 2k (+1)], same per-window layout as
+ * gpu_fft_real_forward. */
+MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len, int32_t n_windows, double *out);
+
+/* =====================================================================
+ * 3. Hot path: batched sliding-window power spectrum over a series
+ *    (shape of gpu_submit_extract_cycles_batch, imports.mqh:14-16;
+ *    nwin = 1 + (series_len - window_len)/hop as at 1.1.0:1016)
+ * ===================================================================== */
+
+/* Window w covers series[w*hop .. w*hop+window_len) of a CHRONOLOGICAL
+ * series (physical memory of an MQL as-series array).  Per window:
+ * detrend -> window -> real FFT -> output.  `out` receives nwin records of
+ * window_len/2 doubles (MTB_OUT_POWER) or window_len doubles
+ * (MTB_OUT_PACKED); only min(nwin, out_cap/record) records are written and
+ * *out_len = records written.  trend_period: InpTrendPeriod (int > 0) for
+ * MTB_DETREND_IIR.  precision: MTB_PREC_F64 or MTB_PREC_F32 (the f32 device
+ * path converts the series to float on the host and results back).
+ * Synchronous. */
+MTB_API int32_t gpu_spectrum_batch(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
+                                   int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
+                                   int32_t output, double *out, int32_t out_cap, int32_t *out_len);
+
+/* Asynchronous form.  Copies `series` before returning (1.1.0:1316 reuses
+ * its buffer right after submit).  *job_id = 0 on failure. */
+MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_len, int32_t window_len,
+                                          int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
+                                          int32_t precision, int32_t output, int64_t *job_id);
+
+/* Poll: MTB_NOT_READY + *ready=0 while pending; MTB_OK + *ready=1 when the
+ * records are copied to out (1.1.0:1032-1035).  Caller frees the job. */
+MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t out_cap, int32_t *out_len,
+                                           int32_t *ready);
+
+/* Kalman 4D parameters for MTB_DETREND_KALMAN, in the order of the inputs
+ * at L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901: follow_strength,
+ * q_pos, q_vel, q_acc, q_jerk, adapt_gain, meas_noise, init_var_pos,
+ * init_var_vel, init_var_acc, init_var_jerk, init_vel, init_acc, init_jerk,
+ * clip_std, ema_blend_period.  n must be 16.  Process-wide. */
+MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
+
+/* =====================================================================
+ * 4. Device-resident plans: the same hot path on buffers already in HBM
+ *    (multi-GPU shards, benchmarks, pipelines that keep data on device).
+ * ===================================================================== */
+
+/* Creates a plan on HIP device `device`.  Returns a handle > 0, or 0 on
+ * error (see gpu_get_last_error_w).  n_windows windows of window_len
+ * samples, window w at offset w*hop (elements) of the series. */
+MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop, int64_t n_windows,
+                                int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
+                                int32_t output);
+
+/* Enqueues the hot path on `hip_stream` (a hipStream_t; NULL = the null
+ * stream) reading d_series (device pointer, double or float per the plan's
+ * precision, >= (n_windows-1)*hop + window_len elements) and writing d_out
+ * (n_windows * record elements).  Asynchronous; no allocation, no sync. */
+MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream);
+
+/* Bytes the plan's algorithm must move per execute: unique input samples
+ * + output, for roofline accounting. */
+MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan);
+
+MTB_API int32_t wsp_plan_destroy(int64_t plan);
+
+/* Version string "mtbridge-mi355x <semver> gfx950" (static storage). */
+MTB_API const char *wsp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTBRIDGE_H */

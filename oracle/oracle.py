@@ -1,0 +1,130 @@
+"""ctypes view of the CPU restatement (wavespec_oracle.c) + numpy helpers.
+
+TEST INFRASTRUCTURE ONLY -- the checker for tests/, __graft_entry__.smoke()
+and the cpu_baseline leg of bench.py.  Never imported by the product
+(fft-wavespec_amd/).  Parity status: "parity unpinned" against the reference
+binary (MQL5 + un-vendored mt-bridge.dll, no reference fixtures); pinned by
+analytic known-answer tests and numpy.fft in tests/test_oracle.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+LIB = ROOT / "build" / "libwavespec_oracle.so"
+DETREND = {"none": 0, "mean": 1, "iir": 2, "kalman": 3}
+WINDOW = {"none": 0, "hann": 1, "hamming": 2, "blackman": 3, "bartlett": 4}
+KALMAN_DEFAULTS = [1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0]
+
+_d = C.POINTER(C.c_double)
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(ROOT)], check=True)
+    return LIB
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        h = C.CDLL(str(LIB))
+        h.ora_fft_manual.argtypes = [_d, C.c_int, _d, _d]
+        h.ora_window_spectrum.argtypes = [_d, C.c_int, C.c_int, C.c_int, C.c_int, _d, C.c_int, _d]
+        h.ora_window_spectrum.restype = C.c_int
+        h.ora_batch_spectrum.argtypes = [_d, C.c_int64, C.c_int, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                         _d, C.c_int, _d]
+        h.ora_batch_spectrum.restype = C.c_int64
+        h.ora_window_value.argtypes = [C.c_int, C.c_int, C.c_int]
+        h.ora_window_value.restype = C.c_double
+        h.ora_detrend_iir.argtypes = [_d, C.c_int, C.c_int, _d]
+        h.ora_detrend_mean.argtypes = [_d, C.c_int, _d]
+        h.ora_kalman_trend.argtypes = [_d, C.c_int, _d, _d]
+        h.ora_gather_series.argtypes = [_d, C.c_int64, C.c_int, _d]
+        _lib = h
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_d)
+
+
+def fft_manual(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """FourierTransformManual (L/WaveSpecZZ_1.0.2.mq5:938-974)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    re, im = np.empty_like(x), np.empty_like(x)
+    lib().ora_fft_manual(_p(x), x.size, _p(re), _p(im))
+    return re, im
+
+
+def window_spectrum(x, detrend="none", window="hann", trend_period=0, kalman=None, output="power") -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    n = x.size
+    out = np.empty(n if output == "packed" else n // 2)
+    kp = None if kalman is None else np.ascontiguousarray(kalman, dtype=np.float64)
+    st = lib().ora_window_spectrum(_p(x), n, DETREND[detrend], WINDOW[window], trend_period,
+                                   None if kp is None else _p(kp), 1 if output == "packed" else 0, _p(out))
+    if st != 0:
+        raise ValueError("oracle rejected the window (N must be a power of two)")
+    return out
+
+
+def batch_spectrum(series, n, hop, detrend="none", window="hann", trend_period=0, kalman=None, output="power",
+                   max_windows=0) -> np.ndarray:
+    """ora_batch_spectrum: window w = series[w*hop : w*hop+n] (OpenMP over windows)."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - n) // hop
+    if max_windows:
+        nwin = min(nwin, max_windows)
+    rec = n if output == "packed" else n // 2
+    out = np.empty((nwin, rec))
+    kp = None if kalman is None else np.ascontiguousarray(kalman, dtype=np.float64)
+    got = lib().ora_batch_spectrum(_p(s), s.size, n, hop, nwin, DETREND[detrend], WINDOW[window], trend_period,
+                                   None if kp is None else _p(kp), 1 if output == "packed" else 0, _p(out))
+    assert got == nwin, (got, nwin)
+    return out
+
+
+# ---------------------------------------------------------------- numpy cross-check
+def numpy_spectrum(x, detrend="none", window="hann", trend_period=0) -> np.ndarray:
+    """Independent numpy restatement (no shared code with the C oracle)."""
+    x = np.asarray(x, dtype=np.float64)
+    n = x.size
+    if detrend == "mean":
+        d = x - x.mean()
+    elif detrend == "iir" and trend_period > 0:
+        om = 2 * np.pi / trend_period
+        al = (1 - np.sin(om)) / np.cos(om)
+        c = (1 - al) / 2
+        t = np.empty(n)
+        prev_x, prev_t = x[0], 0.0
+        for j in range(n):
+            prev_t = c * (x[j] + prev_x) + al * prev_t
+            prev_x = x[j]
+            t[j] = prev_t
+        d = x - t
+    else:
+        d = x.copy()
+    i = np.arange(n)
+    w = {"none": np.ones(n),
+         "hann": 0.5 * (1 - np.cos(2 * np.pi * i / (n - 1))),
+         "hamming": 0.54 - 0.46 * np.cos(2 * np.pi * i / (n - 1)),
+         "blackman": 0.42 - 0.5 * np.cos(2 * np.pi * i / (n - 1)) + 0.08 * np.cos(4 * np.pi * i / (n - 1)),
+         "bartlett": 1 - np.abs((2 * i - n + 1) / (n - 1))}[window]
+    X = np.fft.fft(d * w)[: n // 2]
+    return X.real ** 2 + X.imag ** 2
+
+
+def rel_err(p: np.ndarray, ref: np.ndarray) -> float:
+    """Per-window max_k |P - P_ref| / max_k P_ref, worst over windows."""
+    p = np.atleast_2d(p)
+    ref = np.atleast_2d(ref)
+    den = np.max(np.abs(ref), axis=1)
+    den = np.where(den > 0, den, 1.0)
+    return float(np.max(np.max(np.abs(p - ref), axis=1) / den))

@@ -1,0 +1,231 @@
+"""GPU parity: libmtbridge.so (HIP, gfx950) against the CPU restatement.
+
+Bar: per window
+max_k |P - P_ref| / max_k P_ref <= 1e-10 for fp64 and <= 1e-5 for fp32.
+All calls go through the C ABI.
+"""
+import ctypes as C
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT
+from wavespec_amd import bridge, indicator, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"f64": 1e-10, "f32": 1e-5}
+KALMAN = oracle.KALMAN_DEFAULTS
+
+
+def gpu(series, n, hop, detrend="none", window="hann", period=0, prec="f64", output="power"):
+    return bridge.spectrum_batch(series, n, hop, detrend, window, period, prec, output)
+
+
+def ref(series, n, hop, detrend="none", window="hann", period=0, output="power"):
+    return oracle.batch_spectrum(series, n, hop, detrend, window, period, kalman=KALMAN, output=output)
+
+
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_sizes_hann(gpu_session, n, prec):
+    s = synth.random_walk(37 * n + 11, seed=n)
+    p = gpu(s, n, n, prec=prec)
+    r = ref(s, n, n)
+    assert p.shape == r.shape == (37, n // 2)
+    assert oracle.rel_err(p, r) <= TOL[prec]
+
+
+@pytest.mark.parametrize("n", [64, 1024, 4096])
+@pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024), ("iir", 37), ("kalman", 0)])
+@pytest.mark.parametrize("window", ["none", "hann", "hamming", "blackman", "bartlett"])
+def test_detrend_window_matrix(gpu_session, n, detrend, period, window):
+    s = synth.random_walk(9 * n, seed=3 * n + period)
+    p = gpu(s, n, n, detrend, window, period)
+    r = ref(s, n, n, detrend, window, period)
+    assert oracle.rel_err(p, r) <= TOL["f64"], (detrend, window)
+
+
+@pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024), ("kalman", 0)])
+def test_f32_detrends(gpu_session, detrend, period):
+    n = 4096
+    s = synth.random_walk(6 * n, seed=11)
+    p = gpu(s, n, n, detrend, "hann", period, prec="f32")
+    assert oracle.rel_err(p, ref(s, n, n, detrend, "hann", period)) <= TOL["f32"]
+
+
+@pytest.mark.parametrize("n,hop", [(2048, 1), (1024, 3), (256, 1), (4096, 4097), (512, 700), (64, 1)])
+def test_overlap_and_unaligned_hops(gpu_session, n, hop):
+    """hop=1 (C4 shape, odd offsets -> unaligned loads), hop > N (gaps)."""
+    s = synth.random_walk((150 - 1) * hop + n, seed=13)
+    p = gpu(s, n, hop)
+    r = ref(s, n, hop)
+    assert p.shape[0] == 150
+    assert oracle.rel_err(p, r) <= TOL["f64"]
+
+
+@pytest.mark.parametrize("nwin", [1, 2, 3, 127, 129, 1000])
+def test_ragged_window_counts(gpu_session, nwin):
+    """Window counts that do not fill the last workgroup (2048/M windows per group)."""
+    n = 64
+    s = synth.random_walk(nwin * n, seed=nwin)
+    assert oracle.rel_err(gpu(s, n, n, "mean"), ref(s, n, n, "mean")) <= TOL["f64"]
+
+
+@pytest.mark.parametrize("n", [32, 1024, 4096])
+def test_packed_output(gpu_session, n):
+    s = synth.random_walk(5 * n, seed=5)
+    p = gpu(s, n, n, "none", "hann", output="packed")
+    r = ref(s, n, n, "none", "hann", output="packed")
+    scale = np.max(np.abs(r), axis=1, keepdims=True)
+    assert np.max(np.abs(p - r) / scale) < 1e-12
+    assert np.all(p[:, 1] == 0.0)  # Im X_0
+
+
+def test_fft_real_forward_matches_cpu_fallback(gpu_session):
+    """gpu_fft_real_forward vs FourierTransformManual (the CPU fallback the
+    callers swap it for: L/WaveSpecZZ_1.0.4-new.mq5:3174-3208)."""
+    x = synth.sine_noise_window(1024)
+    out = bridge.fft_real_forward(x)
+    re, im = oracle.fft_manual(x)
+    assert np.max(np.abs(out[0::2] - re[:512])) / np.max(np.abs(re)) < 1e-13
+    assert np.max(np.abs(out[1::2] - im[:512])) / np.max(np.abs(re)) < 1e-13
+
+
+def test_fft_real_forward_batch(gpu_session):
+    w = synth.random_walk(8 * 512, seed=1).reshape(8, 512)
+    out = bridge.fft_real_forward_batch(w)
+    for i in range(8):
+        assert np.allclose(out[i], bridge.fft_real_forward(w[i]), rtol=0, atol=1e-12)
+
+
+def test_out_cap_truncates_records(gpu_session):
+    s = synth.random_walk(10 * 256, seed=2)
+    out = np.full((10, 128), -1.0)
+    got = C.c_int32(0)
+    st = bridge.lib().gpu_spectrum_batch(bridge._dptr(s), s.size, 256, 256, 0, 1, 0, 0, 0, bridge._dptr(out),
+                                         4 * 128 + 5, C.byref(got))
+    assert st == bridge.OK and got.value == 4
+    assert np.all(out[4:] == -1.0)
+    assert oracle.rel_err(out[:4], ref(s, 256, 256)[:4]) <= 1e-10
+
+
+def test_async_job_api(gpu_session):
+    s = synth.random_walk(20000, seed=21)
+    p = indicator.batch_spectra(s, 1024, 1, "iir", "hann", 1024)
+    assert p.shape == (20000 - 1024 + 1, 512)
+    idx = np.r_[0:50, 9000:9050, p.shape[0] - 50:p.shape[0]]
+    r = np.stack([oracle.window_spectrum(s[i:i + 1024], "iir", "hann", 1024) for i in idx])
+    assert oracle.rel_err(p[idx], r) <= 1e-10
+
+
+def test_async_submit_copies_input(gpu_session):
+    s = synth.random_walk(8192, seed=4)
+    keep = s.copy()
+    jid = bridge.submit_spectrum_batch(s, 1024, 1024)
+    s[:] = 0.0  # caller reuses its buffer right after submit (1.1.0:1316)
+    out = np.empty((8, 512))
+    for _ in range(20000):
+        st, ready, n = bridge.try_get_spectrum_batch(jid, out)
+        if ready:
+            break
+    assert st == bridge.OK and ready == 1 and n == 8
+    assert bridge.free_job(jid) == bridge.OK
+    assert bridge.free_job(jid) == bridge.BAD_ARGS
+    assert oracle.rel_err(out, ref(keep, 1024, 1024)) <= 1e-10
+
+
+def test_feed_pipeline_on_calculate(gpu_session, tmp_path):
+    """FeedCache file -> FeedBuilder -> FftProcessor per bar, as 1.1.0 does."""
+    n, bars = 512, 40
+    hist = synth.random_walk(n + bars - 1 + 100, seed=8)
+    close = hist[::-1].copy()  # newest first
+    cache = indicator.FeedCache()
+    ok, delta, _ = indicator.ensure_feed_cache(cache, "EURUSD", "M1", n + bars, True, "WaveSpecZZ",
+                                               lambda start, cnt: close[start:start + cnt], str(tmp_path))
+    assert ok and delta == n + bars
+    spectra = indicator.on_calculate(cache, n, bars)
+    for b in (0, bars // 2, bars - 1):
+        shift = bars - 1 - b
+        win = close[shift:shift + n][::-1]
+        assert oracle.rel_err(spectra[b], oracle.window_spectrum(win, "none", "none")) <= 1e-10
+
+
+@pytest.mark.parametrize("mode", ["live", "batch"])
+def test_cpp_harness(gpu_session, tmp_path, mode):
+    """The C++ MT5 stand-in dlopen()s the library and runs the reference call sequences."""
+    n, bars = 1024, 64
+    hist = synth.random_walk(n + bars - 1, seed=31)
+    feed = tmp_path / "feed.bin"
+    indicator.save_feed_cache(str(feed), hist[::-1].copy())
+    out = tmp_path / "out.bin"
+    r = subprocess.run([str(ROOT / "fft-wavespec_amd" / "bin" / "oncalculate_harness"), str(bridge.LIB_PATH), mode,
+                        str(feed), str(n), str(bars), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    spectra = np.fromfile(out, dtype=np.float64).reshape(bars, n // 2)
+    want = ref(hist, n, 1, "none", "none")
+    assert oracle.rel_err(spectra, want) <= 1e-10
+
+
+def test_plan_device_resident(gpu_session):
+    torch = pytest.importorskip("torch")
+    n, w = 4096, 512
+    dev = torch.device("cuda", 0)
+    s = synth.random_walk(n * w, seed=11)
+    d_s = torch.from_numpy(s).to(dev)
+    d_o = torch.empty(w * n // 2, dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann")
+    assert plan.algorithmic_bytes == (n * w + w * n // 2) * 8
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    p = d_o.cpu().numpy().reshape(w, n // 2)
+    idx = np.r_[0:8, w - 8:w]
+    assert oracle.rel_err(p[idx], ref(s[: (idx[-1] + 1) * n], n, n)[idx]) <= 1e-10
+    plan.close()
+
+
+def test_full_size_properties(gpu_session):
+    """North-star size (65536 x 4096 fp64, 3 GB moved): size-independent
+    properties over ALL windows + oracle parity on a spread sample."""
+    torch = pytest.importorskip("torch")
+    n, w = 4096, 65536
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 11, dev)
+    d_o = torch.empty(w * n // 2, dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "none")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    X = d_s.view(w, n)
+    # Parseval: sum_k |X_k|^2 over k in [0, N/2) relates to the energy; check against torch.fft (fp64)
+    F = torch.fft.rfft(X[::257], dim=1)[:, : n // 2]
+    Pt = F.real ** 2 + F.imag ** 2
+    err = ((P[::257] - Pt).abs().amax(dim=1) / Pt.abs().amax(dim=1)).max().item()
+    assert err < 1e-12
+    assert torch.isfinite(P).all().item() and (P >= 0).all().item()
+    host = d_s.view(w, n)[[0, 12345, w - 1]].cpu().numpy()
+    got = P[[0, 12345, w - 1]].cpu().numpy()
+    for i in range(3):
+        assert oracle.rel_err(got[i], oracle.window_spectrum(host[i], "none", "none")) <= 1e-10
+    plan.close()
+
+
+def test_multi_device_session_shards(gpu_session):
+    """gpu_init(-1): windows sharded over every visible GPU (1 on the test box)."""
+    bridge.shutdown()
+    bridge.init(-1, 16)
+    try:
+        s = synth.random_walk(300 * 512, seed=17)
+        assert oracle.rel_err(gpu(s, 512, 512), ref(s, 512, 512)) <= 1e-10
+    finally:
+        bridge.shutdown()
+        bridge.init(0, 16)
+
+
+@pytest.mark.parametrize("path", sorted((ROOT / "tests" / "golden").glob("*.npz")), ids=lambda p: p.stem)
+def test_golden_vectors_on_gpu(gpu_session, path):
+    g = np.load(path, allow_pickle=False)
+    p = gpu(g["series"], int(g["n"]), int(g["hop"]), str(g["detrend"]), str(g["window"]), int(g["trend_period"]))
+    assert oracle.rel_err(p, g["power"]) <= 1e-10
