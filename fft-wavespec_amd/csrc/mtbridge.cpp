@@ -279,7 +279,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         L.detrend = kDetrendNone;
     }
     L.out = d_out;
-    L.window = t.win;
+    L.window = c.window;
     L.twiddle = t.tw;
     L.n_windows = c.n_windows;
     L.log2n = c.log2n;

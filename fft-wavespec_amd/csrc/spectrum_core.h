@@ -1,0 +1,527 @@
+// spectrum_core.h -- device code of the fused sliding-window power-spectrum
+// kernel for gfx950 (MI355X, CDNA4).  Included by spectrum_kernels.hip (the
+// library's dispatch) and by tools/kbench.hip (ablation variants).
+//
+// One launch = the whole hot path of WaveSpecZZ for a batch of windows:
+//   gather (1.1.0:765-769) -> detrend (none 1.1.0:1239 / mean
+//   L/WaveSpecZZ_gpu_wip.mq5:940-950 / IIR trend L/WaveSpecZZ_1.0.2.mq5:3040-3053)
+//   -> window (L/WaveSpecZZ_1.0.2.mq5:884-935)
+//   -> real FFT (replaces FourierTransformManual L/WaveSpecZZ_1.0.2.mq5:938-974
+//      and the DLL's gpu_fft_real_forward, Include/imports.mqh:7)
+//   -> |X_k|^2, k < N/2 (FftProcessor::Run 1.1.0:529-530) or the packed
+//      out[2k]=Re, out[2k+1]=Im layout (1.1.0:522-528).
+//
+// Design (DESIGN.md "Kernel"):
+//  * A window of N real samples is FFT'd as an M = N/2 point complex FFT of
+//    z[n] = x[2n] + i x[2n+1] plus a real-to-complex post-twiddle; one 16-B
+//    load of (x[2n], x[2n+1]) gives z[n].
+//  * M/16 threads per window, 16 complex points per thread in registers;
+//    Stockham autosort passes of radix 16/8/4/2 with a final radix-8 pass;
+//    LDS only for the transposes between passes: complex AoS, one 16-B
+//    element per ds_read_b128/ds_write_b128, +1 element pad per 16.
+//  * The final pass gives thread t butterflies {t, B-t} (thread 0: {0, B/2}),
+//    so Z[k] and Z[M-k] -- the pair the real post-processing needs -- sit in
+//    the same thread: no extra LDS round trip for the R2C step.
+//  * Each workgroup holds 2048 complex points (1 window at N=4096, 2048/M
+//    windows at smaller N) and walks the batch with a grid-stride loop,
+//    prefetching the next group's samples into registers while it
+//    transforms the current one.
+//  * Window coefficients a0 + a1 cos(th) + a2 cos(2 th), th = 2 pi i/(N-1),
+//    come from a per-thread rotation recurrence (no table traffic).
+//  * Detrend arithmetic is fp64 in both precisions (prices ~1.1 minus a trend
+//    of the same size: fp32 would cancel catastrophically).
+#pragma once
+#include "wsp_internal.h"
+
+namespace wsp {
+namespace core {
+
+template <typename T> struct alignas(2 * sizeof(T)) cpx { T re, im; };
+template <typename T> struct V2;
+// clang ext vectors (not HIP's double2 struct): usable with the nontemporal builtins
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <> struct V2<double> { using t = d2v; };
+template <> struct V2<float> { using t = f2v; };
+
+template <typename T> __device__ __forceinline__ cpx<T> cadd(cpx<T> a, cpx<T> b) { return {a.re + b.re, a.im + b.im}; }
+template <typename T> __device__ __forceinline__ cpx<T> csub(cpx<T> a, cpx<T> b) { return {a.re - b.re, a.im - b.im}; }
+template <typename T> __device__ __forceinline__ cpx<T> cmul(cpx<T> a, cpx<T> b) {
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+template <typename T> __device__ __forceinline__ cpx<T> cconj(cpx<T> a) { return {a.re, -a.im}; }
+
+// cos(2 pi k/16); sin(2 pi k/16) = cos16(k - 4).
+__host__ __device__ constexpr double cos16(int k) {
+    constexpr double C1 = 0.92387953251128675613, C2 = 0.70710678118654752440, C3 = 0.38268343236508977173;
+    switch (k & 15) {
+    case 0: return 1.0;   case 1: return C1;    case 2: return C2;    case 3: return C3;
+    case 4: return 0.0;   case 5: return -C3;   case 6: return -C2;   case 7: return -C1;
+    case 8: return -1.0;  case 9: return -C1;   case 10: return -C2;  case 11: return -C3;
+    case 12: return 0.0;  case 13: return C3;   case 14: return C2;   default: return C1;
+    }
+}
+__host__ __device__ constexpr double sin16(int k) { return cos16(k - 4); }
+
+// a * W16^k, W16 = e^{-2 pi i/16}; k is a compile-time constant after
+// unrolling, so the switch folds and trivial factors cost no multiply.
+template <typename T> __device__ __forceinline__ cpx<T> mulw16(cpx<T> a, int k) {
+    const T h = T(0.70710678118654752440);
+    switch (k & 15) {
+    case 0: return a;
+    case 4: return {a.im, -a.re};
+    case 8: return {-a.re, -a.im};
+    case 12: return {-a.im, a.re};
+    case 2: return {(a.re + a.im) * h, (a.im - a.re) * h};
+    case 6: return {(a.im - a.re) * h, -(a.im + a.re) * h};
+    case 10: return {-(a.re + a.im) * h, (a.re - a.im) * h};
+    case 14: return {(a.re - a.im) * h, (a.im + a.re) * h};
+    default: {
+        const T c = T(cos16(k)), s = T(sin16(k));
+        return {a.re * c + a.im * s, a.im * c - a.re * s};
+    }
+    }
+}
+
+template <int LOG2R> __host__ __device__ constexpr int bitrev(int i) {
+    int r = 0;
+    for (int b = 0; b < LOG2R; ++b) r |= ((i >> b) & 1) << (LOG2R - 1 - b);
+    return r;
+}
+
+// In-register R-point DFT (R = 2,4,8,16), natural order in and out.
+template <typename T, int R> __device__ __forceinline__ void dft(cpx<T> *a) {
+    constexpr int LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+    cpx<T> b[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) b[bitrev<LR>(i)] = a[i];
+#pragma unroll
+    for (int s = 1; s <= LR; ++s) {
+        const int len = 1 << s, half = len >> 1;
+#pragma unroll
+        for (int i = 0; i < R; i += len) {
+#pragma unroll
+            for (int j = 0; j < half; ++j) {
+                const cpx<T> u = b[i + j];
+                const cpx<T> v = mulw16(b[i + j + half], j * (16 / len));
+                b[i + j] = cadd(u, v);
+                b[i + j + half] = csub(u, v);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) a[i] = b[i];
+}
+
+template <int LOG2N> struct Geo {
+    static constexpr int N = 1 << LOG2N;
+    static constexpr int M = N / 2;           // complex points
+    static constexpr int LOG2M = LOG2N - 1;
+    static constexpr int TPW = M / 16;        // threads per window
+    static constexpr int WPB = kBlock / TPW;  // windows per workgroup
+    static constexpr int SLOT = M + M / 16;   // padded complex slots per window
+    static constexpr int Q = LOG2M - 3;
+    static constexpr int N16 = Q / 4, REM = Q % 4;
+    static constexpr int NPASS = N16 + (REM ? 1 : 0) + 1;
+    static constexpr int B = M / 8;           // butterflies of the final radix-8 pass
+    static constexpr int radix(int p) { return p < N16 ? 16 : ((REM && p == N16) ? (1 << REM) : 8); }
+    static constexpr int ns(int p) {
+        int s = 1;
+        for (int i = 0; i < p; ++i) s *= radix(i);
+        return s;
+    }
+    static constexpr int R0 = radix(0);
+    static constexpr int BPT0 = 16 / R0;
+    static_assert(TPW >= 1 && TPW <= kBlock, "window size out of range");
+};
+
+__device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
+__device__ __forceinline__ int pad32(int i) { return i + (i >> 5); }
+// pad16(base + STRIDE*r) written so the per-r part is a compile-time constant
+// (folds into the ds_read/ds_write immediate offset instead of one address
+// VGPR per access): for STRIDE % 16 == 0, pad16(x + 16k) = pad16(x) + 17k.
+template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int base, int r) {
+    if constexpr (STRIDE % 16 == 0) return pbase + (STRIDE / 16) * 17 * r;
+    else return pad16(base + STRIDE * r);
+}
+
+// Window classes: none; a0 + a1 cos th + a2 cos 2th (Hann, Hamming, Blackman);
+// Bartlett (evaluated exactly as L/WaveSpecZZ_1.0.2.mq5:918-922).
+enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2 };
+// Ablation bits (tools/kbench.hip only; the library uses 0).
+enum Var : int { kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8 };
+
+template <typename T> struct SpecArgs {
+    const T *__restrict__ series;
+    T *__restrict__ out;
+    const cpx<T> *__restrict__ tw;  // W_N^k, k < N/2
+    int64_t hop, n_windows, n_groups;
+    int vec;                         // 16-B (8-B for f32) pair loads are aligned
+    int nt;                          // windows do not overlap: stream with non-temporal loads
+    // window: a0 + a1 c + a2 (2c^2 - 1); rotation by step (cs, ss) per r and
+    // by (co, so) from an even to the next odd sample
+    double a0, a1, a2, cs, ss, co, so, inv_theta;  // inv_theta = 2 pi/(N-1)
+    double alpha, c;                 // IIR trend (L/WaveSpecZZ_1.0.2.mq5:3041-3043)
+    double apow[8];                  // alpha^(32 * 2^j)
+};
+
+// Stockham pass p (0 < p < NPASS-1): LDS -> registers -> twiddle -> DFT -> LDS.
+template <typename T, int LOG2N, int PASS>
+__device__ __forceinline__ void mid_pass(cpx<T> *sl, const cpx<T> *__restrict__ tw, int t) {
+    using G = Geo<LOG2N>;
+    constexpr int R = G::radix(PASS), Ns = G::ns(PASS), BPT = 16 / R;
+    constexpr int M = G::M, N = G::N, TPW = G::TPW;
+    cpx<T> v[16];
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) {
+        const int b = t + TPW * q;
+        const int pb = pad16(b);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[q * R + r] = sl[pad16_at<M / R>(pb, b, r)];
+        const cpx<T> w = tw[(b % Ns) * (N / (Ns * R))];
+        cpx<T> wr = w;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+            v[q * R + r] = cmul(v[q * R + r], wr);
+            if (r + 1 < R) wr = cmul(wr, w);
+        }
+        dft<T, R>(&v[q * R]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) {
+        const int b = t + TPW * q;
+        const int base = (b / Ns) * Ns * R + (b % Ns);
+        const int pb = pad16(base);
+#pragma unroll
+        for (int r = 0; r < R; ++r) sl[pad16_at<Ns>(pb, base, r)] = v[q * R + r];
+    }
+    __syncthreads();
+}
+
+template <typename T, int LOG2N, int PASS>
+__device__ __forceinline__ void mid_passes(cpx<T> *sl, const cpx<T> *__restrict__ tw, int t) {
+    if constexpr (PASS < Geo<LOG2N>::NPASS - 1) {
+        mid_pass<T, LOG2N, PASS>(sl, tw, t);
+        mid_passes<T, LOG2N, PASS + 1>(sl, tw, t);
+    }
+}
+
+// Loads the 16 sample pairs of this thread for group g (pass-0 layout,
+// element (q, r) = z[(t + TPW q) + (M/R0) r]).  Inactive slots read window 0.
+template <typename T, int LOG2N, int VAR = 0>
+__device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int slot, int t,
+                                           typename V2<T>::t (&raw)[16]) {
+    using G = Geo<LOG2N>;
+    using v2 = typename V2<T>::t;
+    const int64_t w = g * G::WPB + slot;
+    const T *__restrict__ xw = a.series + (w < a.n_windows ? w : 0) * a.hop;
+    if (a.vec) {
+#pragma unroll
+        for (int q = 0; q < G::BPT0; ++q)
+#pragma unroll
+            for (int r = 0; r < G::R0; ++r)
+            {
+                const v2 *p = reinterpret_cast<const v2 *>(xw + 2 * ((t + G::TPW * q) + (G::M / G::R0) * r));
+                if ((VAR & kVarNtLoad) || a.nt) raw[q * G::R0 + r] = __builtin_nontemporal_load(p);
+                else raw[q * G::R0 + r] = *p;
+            }
+    } else {
+#pragma unroll
+        for (int q = 0; q < G::BPT0; ++q)
+#pragma unroll
+            for (int r = 0; r < G::R0; ++r) {
+                const int n = (t + G::TPW * q) + (G::M / G::R0) * r;
+                raw[q * G::R0 + r].x = xw[2 * n];
+                raw[q * G::R0 + r].y = xw[2 * n + 1];
+            }
+    }
+}
+
+template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
+__global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
+    using G = Geo<LOG2N>;
+    using v2 = typename V2<T>::t;
+    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B;
+    constexpr int R0 = G::R0, BPT0 = G::BPT0;
+    constexpr bool kPrefetch = !(VAR & kVarNoPrefetch);
+    constexpr int kCplx = WPB * SLOT * (int)sizeof(cpx<T>);
+    constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
+    constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
+    constexpr int kScan = 16 * 8;
+    __shared__ __attribute__((aligned(16))) char smem[kMain + kScan];
+    double *scanbuf = reinterpret_cast<double *>(smem + kMain);
+
+    const int tid = threadIdx.x;
+    const int slot = tid / TPW;
+    const int t = tid % TPW;
+    cpx<T> *sl = reinterpret_cast<cpx<T> *>(smem) + slot * SLOT;
+
+    // per-thread window rotation start: th_i at i = 2 (t + TPW q)
+    double wc0[BPT0], ws0[BPT0];
+    if constexpr (WCLASS == kWinCos) {
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q) sincos(a.inv_theta * (double)(2 * (t + TPW * q)), &ws0[q], &wc0[q]);
+    }
+
+    v2 raw[16];
+    int64_t g = blockIdx.x;
+    if (kPrefetch && g < a.n_groups) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
+
+    for (; g < a.n_groups; g += gridDim.x) {
+        const int64_t w = g * WPB + slot;
+        const bool active = w < a.n_windows;
+        if (!kPrefetch) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
+        double xa[16], xb[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            xa[i] = (double)raw[i].x;
+            xb[i] = (double)raw[i].y;
+        }
+        if (kPrefetch && g + gridDim.x < a.n_groups) load_group<T, LOG2N, VAR>(a, g + gridDim.x, slot, t, raw);
+
+        // ---- detrend (fp64)
+        if constexpr (DETREND == kDetrendMean) {
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s += xa[i] + xb[i];
+            constexpr int SW = TPW < 64 ? TPW : 64;
+#pragma unroll
+            for (int off = SW / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, SW);
+            if constexpr (TPW == 128) {
+                __syncthreads();  // scanbuf reuse across groups
+                if ((tid & 63) == 0) scanbuf[tid >> 6] = s;
+                __syncthreads();
+                s = scanbuf[0] + scanbuf[1];
+            }
+            const double mean = s / (double)N;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                xa[i] -= mean;
+                xb[i] -= mean;
+            }
+        } else if constexpr (DETREND == kDetrendIir) {
+            // t0 = c(x0+x0), tj = c(xj+x(j-1)) + alpha t(j-1), d = x - t.
+            // Chunk of 32 samples per thread, affine carry scan across threads.
+            double *rawl = reinterpret_cast<double *>(smem) + slot * (N + N / 32);
+            __syncthreads();  // previous group's LDS reads are complete
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int n = (t + TPW * q) + (M / R0) * r;
+                    rawl[pad32(2 * n)] = xa[q * R0 + r];
+                    rawl[pad32(2 * n + 1)] = xb[q * R0 + r];
+                }
+            __syncthreads();
+            const double alpha = a.alpha, c = a.c;
+            double xc[33];
+            xc[0] = rawl[pad32(t == 0 ? 0 : 32 * t - 1)];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) xc[j + 1] = rawl[pad32(32 * t + j)];
+            double tr = 0.0;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) tr = c * (xc[j + 1] + xc[j]) + alpha * tr;
+            // inclusive scan: v_t = sum_{s<=t} alpha^(32(t-s)) e_s
+            constexpr int SW = TPW < 64 ? TPW : 64;
+            const int lt = t & (SW - 1);
+            double v = tr;
+#pragma unroll
+            for (int j = 0, d = 1; d < SW; ++j, d <<= 1) {
+                const double up = __shfl_up(v, d, SW);
+                if (lt >= d) v = a.apow[j] * up + v;
+            }
+            double carry = __shfl_up(v, 1, SW);
+            if constexpr (TPW == 128) {
+                if (t == 63) scanbuf[0] = v;
+                __syncthreads();
+                if (t >= 64) {
+                    const double v0 = scanbuf[0];
+                    double p = 1.0;
+                    const int m = lt + 1;
+#pragma unroll
+                    for (int j = 0; j < 7; ++j)
+                        if ((m >> j) & 1) p *= a.apow[j];
+                    v = p * v0 + v;
+                    carry = __shfl_up(v, 1, SW);
+                    if (lt == 0) carry = v0;
+                }
+            }
+            if (t == 0) carry = 0.0;
+            tr = carry;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                tr = c * (xc[j + 1] + xc[j]) + alpha * tr;
+                rawl[pad32(32 * t + j)] = xc[j + 1] - tr;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int n = (t + TPW * q) + (M / R0) * r;
+                    xa[q * R0 + r] = rawl[pad32(2 * n)];
+                    xb[q * R0 + r] = rawl[pad32(2 * n + 1)];
+                }
+        }
+
+        // ---- window (fp64) + pass 0 (no twiddles: Ns = 1)
+        cpx<T> v[16];
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q) {
+            double c = 0.0, s = 0.0;
+            if constexpr (WCLASS == kWinCos) {
+                c = wc0[q];
+                s = ws0[q];
+                asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no 64-VGPR hoist
+            }
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                double da = xa[q * R0 + r], db = xb[q * R0 + r];
+                if constexpr (WCLASS == kWinCos) {
+                    const double co = c * a.co - s * a.so;  // th_(i+1)
+                    da *= a.a0 + a.a1 * c + a.a2 * (2.0 * c * c - 1.0);
+                    db *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                    const double cn = c * a.cs - s * a.ss;
+                    s = s * a.cs + c * a.ss;
+                    c = cn;
+                } else if constexpr (WCLASS == kWinBartlett) {
+                    const int i = 2 * ((t + TPW * q) + (M / R0) * r);
+                    da *= 1.0 - fabs((2.0 * i - N + 1) / (N - 1));
+                    db *= 1.0 - fabs((2.0 * (i + 1) - N + 1) / (N - 1));
+                }
+                v[q * R0 + r] = {T(da), T(db)};
+            }
+        }
+
+        if constexpr (VAR & kVarSkeleton) {
+            // memory-pattern ablation: same loads and stores, no transform
+            if (active) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int k = (q == 0 ? t : (t == 0 ? TPW : 2 * TPW - t)) + B * r;
+                        a.out[w * M + k] = v[q * 8 + r].re + v[q * 8 + r].im;
+                    }
+            }
+            continue;
+        }
+
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q) dft<T, R0>(&v[q * R0]);
+        __syncthreads();  // previous group's final-pass LDS reads are done
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q) {
+            const int b = t + TPW * q;
+            // R0 consecutive elements: pad16(b R0 + r) = pad16(b R0) + r when
+            // b R0 % 16 + r < 16 (always for R0 = 16; r < R0 divides 16)
+            const int pb = pad16(b * R0);
+#pragma unroll
+            for (int r = 0; r < R0; ++r) sl[pb + r] = v[q * R0 + r];
+        }
+        __syncthreads();
+
+        // ---- middle passes
+        mid_passes<T, LOG2N, 1>(sl, a.tw, t);
+
+        // ---- final radix-8 pass: thread t owns butterflies {t, B-t} ({0, B/2} for t = 0)
+        const int bq0 = t, bq1 = t == 0 ? TPW : 2 * TPW - t;
+        cpx<T> u0[8], u1[8];
+        const int pq0 = pad16(bq0), pq1 = pad16(bq1);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            u0[r] = sl[pad16_at<B>(pq0, bq0, r)];
+            u1[r] = sl[pad16_at<B>(pq1, bq1, r)];
+        }
+        if constexpr (G::NPASS > 1) {
+            const cpx<T> w0 = a.tw[2 * bq0], w1 = a.tw[2 * bq1];  // (b % Ns) * N/(Ns*8) with Ns = B
+            cpx<T> wr0 = w0, wr1 = w1;
+#pragma unroll
+            for (int r = 1; r < 8; ++r) {
+                u0[r] = cmul(u0[r], wr0);
+                u1[r] = cmul(u1[r], wr1);
+                if (r + 1 < 8) {
+                    wr0 = cmul(wr0, w0);
+                    wr1 = cmul(wr1, w1);
+                }
+            }
+        }
+        dft<T, 8>(u0);
+        dft<T, 8>(u1);
+        // u0[r] = Z[t + B r], u1[r] = Z[(B - t) + B r] = conj-partner of u0[7 - r].
+        // Thread 0 holds Z[B r] and Z[B/2 + B r]; permute it into the same
+        // slot pattern (slot s pairs u0[s] with u1[7-s], M - k_A = k_B).
+        if (t == 0) {
+            cpx<T> n0[8], n1[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                n0[r] = u1[r];           // k = B/2 + B r   <->  u1[7-r]
+                n0[4 + r] = u0[r];       // k = B r  (slot 4: Z[0], special)
+                n1[4 + r] = u1[4 + r];
+            }
+            n1[0] = u0[5];               // partner of u0[3]: B*5 = M - 3B
+            n1[1] = u0[6];
+            n1[2] = u0[7];
+            n1[3] = u0[4];               // slot 4 partner: Z[M/2] (special)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                u0[r] = n0[r];
+                u1[r] = n1[r];
+            }
+        }
+
+        // ---- real-to-complex post-processing + |X|^2, one slot per (k, M-k):
+        // E = (Z[k] + conj Z[M-k])/2, O = -i (Z[k] - conj Z[M-k])/2,
+        // X[k] = E + W_N^k O, X[M-k] = conj(E - W_N^k O).
+        const cpx<T> wt = a.tw[t];
+        const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
+        const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
+        if (active) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const cpx<T> A = u0[s], Bv = u1[7 - s];
+                const cpx<T> wk = mulw16(s < 4 ? wlo : whi, s);
+                const cpx<T> e = {A.re + Bv.re, A.im - Bv.im};
+                const cpx<T> o = {A.im + Bv.im, Bv.re - A.re};
+                const cpx<T> wo = cmul(wk, o);
+                cpx<T> xa = cadd(e, wo);               // 2 X[k_A]
+                cpx<T> xb = {e.re - wo.re, wo.im - e.im};  // 2 X[M - k_A]
+                int ka = t + B * s, kb = M - ka;
+                if (t == 0) {
+                    ka = s < 4 ? B / 2 + B * s : B * (s - 4);
+                    kb = s == 4 ? M / 2 : M - ka;
+                    if (s == 4) {  // self-paired bins: X[0] real, X[M/2] = conj Z[M/2]
+                        xa = {T(2) * (A.re + A.im), T(0)};
+                        xb = {T(2) * Bv.re, T(-2) * Bv.im};
+                    }
+                }
+                if constexpr (OUT == kOutPower) {
+                    const T pa = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
+                    const T pb = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+                    if constexpr (VAR & kVarNtStore) {
+                        __builtin_nontemporal_store(pa, a.out + w * M + ka);
+                        __builtin_nontemporal_store(pb, a.out + w * M + kb);
+                    } else {
+                        a.out[w * M + ka] = pa;
+                        a.out[w * M + kb] = pb;
+                    }
+                } else {
+                    v2 oa, ob;
+                    oa.x = T(0.5) * xa.re;
+                    oa.y = T(0.5) * xa.im;
+                    ob.x = T(0.5) * xb.re;
+                    ob.y = T(0.5) * xb.im;
+                    *reinterpret_cast<v2 *>(a.out + w * N + 2 * ka) = oa;
+                    *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
+                }
+            }
+        }
+    }
+}
+
+// Host-side argument setup shared by the library and the tools.
+template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb);
+
+}  // namespace core
+}  // namespace wsp

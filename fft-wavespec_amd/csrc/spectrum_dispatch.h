@@ -1,0 +1,111 @@
+// spectrum_dispatch.h -- host-side argument setup and template dispatch of
+// the spectrum kernel (one instantiation per N, detrend, output, window class).
+#pragma once
+#include <cmath>
+
+#include "spectrum_core.h"
+
+namespace wsp {
+namespace core {
+
+// Window coefficients of L/WaveSpecZZ_1.0.2.mq5:884-922 as a0 + a1 cos th + a2 cos 2th.
+inline int window_class(int window, double *a0, double *a1, double *a2) {
+    *a0 = 1.0, *a1 = 0.0, *a2 = 0.0;
+    switch (window) {
+    case 1: *a0 = 0.5, *a1 = -0.5; return kWinCos;                  // Hann 0.5(1 - cos)
+    case 2: *a0 = 0.54, *a1 = -0.46; return kWinCos;                // Hamming
+    case 3: *a0 = 0.42, *a1 = -0.5, *a2 = 0.08; return kWinCos;     // Blackman
+    case 4: return kWinBartlett;
+    default: return kWinNone;
+    }
+}
+
+template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
+    SpecArgs<T> a{};
+    a.series = static_cast<const T *>(L.series);
+    a.out = static_cast<T *>(L.out);
+    a.tw = static_cast<const cpx<T> *>(L.twiddle);
+    a.hop = L.hop;
+    a.n_windows = L.n_windows;
+    a.n_groups = (L.n_windows + wpb - 1) / wpb;
+    a.vec = (L.hop % 2 == 0) && (reinterpret_cast<uintptr_t>(L.series) % (2 * sizeof(T)) == 0);
+    // overlapping windows re-read samples from L2/MALL: keep them cacheable
+    a.nt = L.nt_mode == 2 || (L.nt_mode == 0 && L.hop >= (int64_t(1) << L.log2n));
+    window_class(L.window, &a.a0, &a.a1, &a.a2);
+    const int n = 1 << L.log2n;
+    const int m = n / 2;
+    const int log2m = L.log2n - 1;
+    const int q = log2m - 3;
+    const int r0 = q / 4 > 0 ? 16 : (q % 4 ? (1 << (q % 4)) : 8);
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    const long double th = two_pi / (long double)(n - 1);
+    a.inv_theta = (double)th;
+    a.cs = (double)cosl(th * (long double)(2 * (m / r0)));
+    a.ss = (double)sinl(th * (long double)(2 * (m / r0)));
+    a.co = (double)cosl(th);
+    a.so = (double)sinl(th);
+    a.alpha = L.iir_alpha;
+    a.c = L.iir_c;
+    for (int j = 0; j < 8; ++j) a.apow[j] = L.iir_apow[j];
+    return a;
+}
+
+// Library default: no register prefetch (measured slower at 2 waves/SIMD:
+// profiles/README.md, kbench rounds) and a 16384-workgroup grid-stride launch.
+constexpr int kDefaultVar = kVarNoPrefetch;
+constexpr int kDefaultGrid = 16384;
+
+template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = kDefaultVar>
+hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
+    using G = Geo<LOG2N>;
+    const SpecArgs<T> a = make_args<T>(L, G::WPB);
+    int64_t grid = L.grid > 0 ? L.grid : kDefaultGrid;
+    if (grid > a.n_groups) grid = a.n_groups;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((spectrum_kernel<T, LOG2N, DETREND, OUT, WCLASS, VAR>), dim3((unsigned)grid), dim3(kBlock),
+                       0, stream, a);
+    return hipGetLastError();
+}
+
+template <typename T, int LOG2N, int DETREND, int OUT>
+hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
+    double a0, a1, a2;
+    switch (window_class(L.window, &a0, &a1, &a2)) {
+    case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos>(L, s);
+    case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett>(L, s);
+    default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone>(L, s);
+    }
+}
+
+template <typename T, int LOG2N, int DETREND>
+hipError_t dispatch_out(const SpectrumLaunch &L, hipStream_t s) {
+    return L.output == kOutPacked ? dispatch_win<T, LOG2N, DETREND, kOutPacked>(L, s)
+                                  : dispatch_win<T, LOG2N, DETREND, kOutPower>(L, s);
+}
+
+template <typename T, int LOG2N> hipError_t dispatch_detrend(const SpectrumLaunch &L, hipStream_t s) {
+    switch (L.detrend) {
+    case kDetrendNone: return dispatch_out<T, LOG2N, kDetrendNone>(L, s);
+    case kDetrendMean: return dispatch_out<T, LOG2N, kDetrendMean>(L, s);
+    case kDetrendIir: return dispatch_out<T, LOG2N, kDetrendIir>(L, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename T> hipError_t dispatch_n(const SpectrumLaunch &L, hipStream_t s) {
+    if (L.n_windows <= 0) return hipSuccess;
+    switch (L.log2n) {
+    case 5: return dispatch_detrend<T, 5>(L, s);
+    case 6: return dispatch_detrend<T, 6>(L, s);
+    case 7: return dispatch_detrend<T, 7>(L, s);
+    case 8: return dispatch_detrend<T, 8>(L, s);
+    case 9: return dispatch_detrend<T, 9>(L, s);
+    case 10: return dispatch_detrend<T, 10>(L, s);
+    case 11: return dispatch_detrend<T, 11>(L, s);
+    case 12: return dispatch_detrend<T, 12>(L, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace core
+}  // namespace wsp

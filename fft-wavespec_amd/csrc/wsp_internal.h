@@ -21,8 +21,8 @@ enum Output : int { kOutPower = 0, kOutPacked = 1 };
 struct SpectrumLaunch {
     const void *series;   // window w starts at series + w*hop (elements)
     void *out;            // n_windows records of N/2 (power) or N (packed)
-    const void *window;   // N window coefficients (element type), or null = rectangular
     const void *twiddle;  // N/2 complex W_N^k, element type
+    int window;           // MTB_WINDOW_* (enum WINDOW_TYPE, L/WaveSpecZZ_1.0.2.mq5:626-632)
     int64_t hop;
     int64_t n_windows;
     int log2n;
@@ -33,9 +33,11 @@ struct SpectrumLaunch {
     double iir_alpha, iir_c;
     double iir_apow[8];   // alpha^(32 * 2^j), j = 0..7
     int grid;             // 0 = auto
+    int nt_mode;          // non-temporal sample loads: 0 = auto (hop >= N), 1 = off, 2 = on
 };
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);
+hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t stream);
 
 // Per-window Kalman 4D detrend pre-pass: d[w*N + j] = x_j - trend_j
 // (one lane per window; trend arithmetic in fp64 like the MQL5 source).

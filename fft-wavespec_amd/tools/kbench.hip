@@ -1,0 +1,174 @@
+// kbench.hip -- ablation micro-benchmark for the spectrum kernel (not part
+// of the library).  One process, interleaved rounds (cdna_hip_programming.md
+// sec. 5.4 rule 24): variants of the same kernel, a 2:1 read/write copy
+// kernel as the practical HBM ceiling for this traffic shape, grid sweeps.
+//
+//   kbench [log2n=12] [windows=65536] [reps=20] [rounds=3]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../csrc/spectrum_dispatch.h"
+
+using namespace wsp;
+using namespace wsp::core;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e), __FILE__, __LINE__); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+__global__ void fill_walk(double *x, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 32;
+        x[i] = 1.1 + 1e-3 * ((double)(h >> 11) * (1.0 / 9007199254740992.0) - 0.5) + 0.002 * sin(0.1256 * (double)i);
+    }
+}
+
+// 1:1 float4 copy (calibration against MI355X_MICROARCH.md: 6.29 TB/s)
+__global__ __launch_bounds__(256) void copy11(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        out[j] = in[j];
+}
+
+// 2:1 with 4 independent loads in flight per thread, optional nt stores
+template <bool NT>
+__global__ __launch_bounds__(256) void copy21u(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n_out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_out; j += 2 * stride) {
+        const bool two = j + stride < n_out;
+        const double2 a = in[2 * j], b = in[2 * j + 1];
+        double2 c = a, d = b;
+        if (two) { c = in[2 * (j + stride)]; d = in[2 * (j + stride) + 1]; }
+        const double2 o0 = make_double2(a.x + b.x, a.y + b.y), o1 = make_double2(c.x + d.x, c.y + d.y);
+        if (NT) {
+            __builtin_nontemporal_store(d2v{o0.x, o0.y}, reinterpret_cast<d2v *>(out + j));
+            if (two) __builtin_nontemporal_store(d2v{o1.x, o1.y}, reinterpret_cast<d2v *>(out + j + stride));
+        }
+        else { out[j] = o0; if (two) out[j + stride] = o1; }
+    }
+}
+
+// 2:1 read:write streaming kernel (the spectrum's traffic shape, no compute)
+__global__ __launch_bounds__(256) void copy21(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n_out) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_out; j += (int64_t)gridDim.x * blockDim.x) {
+        const double2 a = in[2 * j], b = in[2 * j + 1];
+        out[j] = make_double2(a.x + b.x, a.y + b.y);
+    }
+}
+
+template <int VAR>
+float time_variant(const SpectrumLaunch &L, hipStream_t s, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 2; ++i) CK((launch_one<double, 12, kDetrendNone, kOutPower, kWinCos, VAR>(L, s)));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i) CK((launch_one<double, 12, kDetrendNone, kOutPower, kWinCos, VAR>(L, s)));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return ms * 1000.f / reps;
+}
+
+int main(int argc, char **argv) {
+    const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+    const int n = 4096;
+    const int64_t len = W * n;
+    double *x, *out, *tw;
+    CK(hipMalloc(&x, len * 8));
+    CK(hipMalloc(&out, W * n / 2 * 8));
+    CK(hipMalloc(&tw, n / 2 * 16));
+    std::vector<double> h(n);
+    for (int k = 0; k < n / 2; ++k) {
+        long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+        h[2 * k] = (double)cosl(a);
+        h[2 * k + 1] = (double)sinl(a);
+    }
+    CK(hipMemcpy(tw, h.data(), n * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_walk, dim3(4096), dim3(256), 0, 0, x, len);
+    CK(hipDeviceSynchronize());
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+
+    SpectrumLaunch L{};
+    L.series = x;
+    L.out = out;
+    L.twiddle = tw;
+    L.window = 1;
+    L.hop = n;
+    L.n_windows = W;
+    L.log2n = 12;
+    L.output = 0;
+    L.nt_mode = 1;  // variants choose nt loads via VAR (kVarNtLoad)
+    const double bytes = (double)len * 8 + (double)W * n / 2 * 8;
+    printf("# W=%lld N=%d algorithmic bytes=%.3f GB, roofline(8 TB/s)=%.1f us\n", (long long)W, n, bytes / 1e9,
+           bytes / 8e12 * 1e6);
+
+    const int grids[] = {256, 1024, 4096, 8192, 16384, 65536};
+    for (int round = 0; round < rounds; ++round) {
+        // copy ceiling
+        {
+            hipEvent_t e0, e1;
+            CK(hipEventCreate(&e0));
+            CK(hipEventCreate(&e1));
+            for (int kind = 0; kind < 4; ++kind)
+                for (int g : {1024, 2048, 8192}) {
+                    auto go = [&] {
+                        if (kind == 0)  // 1:1 copy of out-sized region x2 (same bytes: read 2/3, write... see below)
+                            hipLaunchKernelGGL(copy11, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
+                        else if (kind == 1)
+                            hipLaunchKernelGGL(copy21, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
+                        else if (kind == 2)
+                            hipLaunchKernelGGL(copy21u<false>, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
+                        else
+                            hipLaunchKernelGGL(copy21u<true>, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
+                    };
+                    go();
+                    CK(hipEventRecord(e0, s));
+                    for (int i = 0; i < reps; ++i) go();
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    const double us = ms * 1000.0 / reps;
+                    const double b = kind == 0 ? (double)len / 4 * 32 : bytes;  // copy11 moves 16 B in + 16 B out per elem
+                    const char *nm[] = {"copy11", "copy21", "copy21u", "copy21u-nt"};
+                    printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s\n", round, nm[kind], g, us, b / us / 1e3);
+                }
+        }
+        for (int g : grids) {
+            L.grid = g;
+            struct {
+                const char *name;
+                float us;
+            } r[6] = {{"pf", time_variant<0>(L, s, reps)},
+                      {"nopf", time_variant<kVarNoPrefetch>(L, s, reps)},
+                      {"nopf+ntld", time_variant<kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
+                      {"nopf+ntst", time_variant<kVarNoPrefetch | kVarNtStore>(L, s, reps)},
+                      {"nopf+nt2", time_variant<kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"skel", time_variant<kVarSkeleton | kVarNoPrefetch>(L, s, reps)}};
+            for (auto &v : r)
+                printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s  %.3f of 8TB/s\n", round, v.name, g, v.us,
+                       bytes / v.us / 1e3, bytes / v.us / 1e3 / 8000.0);
+        }
+        fflush(stdout);
+    }
+    return 0;
+}
