@@ -149,7 +149,7 @@ template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int bas
 // Bartlett (evaluated exactly as L/WaveSpecZZ_1.0.2.mq5:918-922).
 enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2 };
 // Ablation bits (tools/kbench.hip only; the library uses 0).
-enum Var : int { kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8 };
+enum Var : int { kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32 };
 
 template <typename T> struct SpecArgs {
     const T *__restrict__ series;
@@ -264,11 +264,19 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
         for (int q = 0; q < BPT0; ++q) sincos(a.inv_theta * (double)(2 * (t + TPW * q)), &ws0[q], &wc0[q]);
     }
 
-    v2 raw[16];
-    int64_t g = blockIdx.x;
-    if (kPrefetch && g < a.n_groups) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
+    // group sequence of this workgroup: cyclic (g = b + i*grid, the default:
+    // the chip's in-flight windows stay one contiguous region) or blocked
+    constexpr bool kBlocked = VAR & kVarBlocked;
+    const int64_t per = kBlocked ? (a.n_groups + gridDim.x - 1) / gridDim.x : 0;
+    const int64_t g_first = kBlocked ? (int64_t)blockIdx.x * per : (int64_t)blockIdx.x;
+    const int64_t g_step = kBlocked ? 1 : (int64_t)gridDim.x;
+    const int64_t g_end = kBlocked ? (g_first + per < a.n_groups ? g_first + per : a.n_groups) : a.n_groups;
 
-    for (; g < a.n_groups; g += gridDim.x) {
+    v2 raw[16];
+    int64_t g = g_first;
+    if (kPrefetch && g < g_end) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
+
+    for (; g < g_end; g += g_step) {
         const int64_t w = g * WPB + slot;
         const bool active = w < a.n_windows;
         if (!kPrefetch) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
             xa[i] = (double)raw[i].x;
             xb[i] = (double)raw[i].y;
         }
-        if (kPrefetch && g + gridDim.x < a.n_groups) load_group<T, LOG2N, VAR>(a, g + gridDim.x, slot, t, raw);
+        if (kPrefetch && g + g_step < g_end) load_group<T, LOG2N, VAR>(a, g + g_step, slot, t, raw);
 
         // ---- detrend (fp64)
         if constexpr (DETREND == kDetrendMean) {
@@ -394,6 +402,19 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
             }
         }
 
+        if constexpr (VAR & kVarSkelWide) {
+            // memory-pattern ablation with 16-B contiguous stores
+            if (active) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    v2 o;
+                    o.x = v[2 * j].re + v[2 * j].im;
+                    o.y = v[2 * j + 1].re + v[2 * j + 1].im;
+                    *reinterpret_cast<v2 *>(a.out + w * M + 2 * (t + TPW * j)) = o;
+                }
+            }
+            continue;
+        }
         if constexpr (VAR & kVarSkeleton) {
             // memory-pattern ablation: same loads and stores, no transform
             if (active) {
@@ -477,43 +498,51 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
         const cpx<T> wt = a.tw[t];
         const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
-        if (active) {
+        T *prow = reinterpret_cast<T *>(sl);  // power row staged in this window's LDS slot
+        if constexpr (OUT == kOutPower) __syncthreads();  // every final-pass LDS read is done
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const cpx<T> A = u0[s], Bv = u1[7 - s];
-                const cpx<T> wk = mulw16(s < 4 ? wlo : whi, s);
-                const cpx<T> e = {A.re + Bv.re, A.im - Bv.im};
-                const cpx<T> o = {A.im + Bv.im, Bv.re - A.re};
-                const cpx<T> wo = cmul(wk, o);
-                cpx<T> xa = cadd(e, wo);               // 2 X[k_A]
-                cpx<T> xb = {e.re - wo.re, wo.im - e.im};  // 2 X[M - k_A]
-                int ka = t + B * s, kb = M - ka;
-                if (t == 0) {
-                    ka = s < 4 ? B / 2 + B * s : B * (s - 4);
-                    kb = s == 4 ? M / 2 : M - ka;
-                    if (s == 4) {  // self-paired bins: X[0] real, X[M/2] = conj Z[M/2]
-                        xa = {T(2) * (A.re + A.im), T(0)};
-                        xb = {T(2) * Bv.re, T(-2) * Bv.im};
-                    }
+        for (int s = 0; s < 8; ++s) {
+            const cpx<T> A = u0[s], Bv = u1[7 - s];
+            const cpx<T> wk = mulw16(s < 4 ? wlo : whi, s);
+            const cpx<T> e = {A.re + Bv.re, A.im - Bv.im};
+            const cpx<T> o = {A.im + Bv.im, Bv.re - A.re};
+            const cpx<T> wo = cmul(wk, o);
+            cpx<T> xa = cadd(e, wo);                   // 2 X[k_A]
+            cpx<T> xb = {e.re - wo.re, wo.im - e.im};  // 2 X[M - k_A]
+            int ka = t + B * s, kb = M - ka;
+            if (t == 0) {
+                ka = s < 4 ? B / 2 + B * s : B * (s - 4);
+                kb = s == 4 ? M / 2 : M - ka;
+                if (s == 4) {  // self-paired bins: X[0] real, X[M/2] = conj Z[M/2]
+                    xa = {T(2) * (A.re + A.im), T(0)};
+                    xb = {T(2) * Bv.re, T(-2) * Bv.im};
                 }
-                if constexpr (OUT == kOutPower) {
-                    const T pa = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
-                    const T pb = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
-                    if constexpr (VAR & kVarNtStore) {
-                        __builtin_nontemporal_store(pa, a.out + w * M + ka);
-                        __builtin_nontemporal_store(pb, a.out + w * M + kb);
-                    } else {
-                        a.out[w * M + ka] = pa;
-                        a.out[w * M + kb] = pb;
-                    }
-                } else {
-                    v2 oa, ob;
-                    oa.x = T(0.5) * xa.re;
-                    oa.y = T(0.5) * xa.im;
-                    ob.x = T(0.5) * xb.re;
-                    ob.y = T(0.5) * xb.im;
-                    *reinterpret_cast<v2 *>(a.out + w * N + 2 * ka) = oa;
-                    *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
+            }
+            if constexpr (OUT == kOutPower) {
+                prow[ka] = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
+                prow[kb] = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+            } else if (active) {  // packed: (Re, Im) of one bin is already one 16-B (8-B) store
+                v2 oa, ob;
+                oa.x = T(0.5) * xa.re;
+                oa.y = T(0.5) * xa.im;
+                ob.x = T(0.5) * xb.re;
+                ob.y = T(0.5) * xb.im;
+                *reinterpret_cast<v2 *>(a.out + w * N + 2 * ka) = oa;
+                *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
+            }
+        }
+        if constexpr (OUT == kOutPower) {
+            // write the row back with contiguous 16-B stores (1 KiB per wave instruction)
+            constexpr int VE = 16 / (int)sizeof(T);
+            typedef T vst __attribute__((ext_vector_type(16 / sizeof(T))));
+            __syncthreads();
+            if (active) {
+#pragma unroll
+                for (int j = 0; j < 16 / VE; ++j) {
+                    const int k = VE * (t + TPW * j);
+                    const vst val = *reinterpret_cast<const vst *>(prow + k);
+                    if constexpr (VAR & kVarNtStore) __builtin_nontemporal_store(val, reinterpret_cast<vst *>(a.out + w * M + k));
+                    else *reinterpret_cast<vst *>(a.out + w * M + k) = val;
                 }
             }
         }

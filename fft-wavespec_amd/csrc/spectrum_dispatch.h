@@ -50,9 +50,11 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     return a;
 }
 
-// Library default: no register prefetch (measured slower at 2 waves/SIMD:
-// profiles/README.md, kbench rounds) and a 16384-workgroup grid-stride launch.
-constexpr int kDefaultVar = kVarNoPrefetch;
+// Library default (profiles/r01/kbench_*.log, interleaved rounds): no register
+// prefetch (slower at the LDS-limited 2 waves/SIMD), non-temporal 16-B stores
+// of the LDS-staged power row, a 16384-workgroup grid-stride launch.  The
+// sample loads are non-temporal only when windows do not overlap (a.nt).
+constexpr int kDefaultVar = kVarNoPrefetch | kVarNtStore;
 constexpr int kDefaultGrid = 16384;
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = kDefaultVar>

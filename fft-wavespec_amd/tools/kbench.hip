@@ -42,6 +42,18 @@ __global__ __launch_bounds__(256) void copy11(const double2 *__restrict__ in, do
         out[j] = in[j];
 }
 
+// 1:1 copy, 4 float4 in flight per thread
+__global__ __launch_bounds__(256) void copy11x4(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j + 3 * stride < n; j += 4 * stride) {
+        const double2 a = in[j], b = in[j + stride], c = in[j + 2 * stride], d = in[j + 3 * stride];
+        out[j] = a;
+        out[j + stride] = b;
+        out[j + 2 * stride] = c;
+        out[j + 3 * stride] = d;
+    }
+}
+
 // 2:1 with 4 independent loads in flight per thread, optional nt stores
 template <bool NT>
 __global__ __launch_bounds__(256) void copy21u(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n_out) {
@@ -121,14 +133,14 @@ int main(int argc, char **argv) {
     printf("# W=%lld N=%d algorithmic bytes=%.3f GB, roofline(8 TB/s)=%.1f us\n", (long long)W, n, bytes / 1e9,
            bytes / 8e12 * 1e6);
 
-    const int grids[] = {256, 1024, 4096, 8192, 16384, 65536};
+    const int grids[] = {1024, 4096, 8192, 16384, 32768, 65536};
     for (int round = 0; round < rounds; ++round) {
         // copy ceiling
         {
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0));
             CK(hipEventCreate(&e1));
-            for (int kind = 0; kind < 4; ++kind)
+            for (int kind = 0; kind < 5; ++kind)
                 for (int g : {1024, 2048, 8192}) {
                     auto go = [&] {
                         if (kind == 0)  // 1:1 copy of out-sized region x2 (same bytes: read 2/3, write... see below)
@@ -137,8 +149,10 @@ int main(int argc, char **argv) {
                             hipLaunchKernelGGL(copy21, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
                         else if (kind == 2)
                             hipLaunchKernelGGL(copy21u<false>, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
-                        else
+                        else if (kind == 3)
                             hipLaunchKernelGGL(copy21u<true>, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
+                        else
+                            hipLaunchKernelGGL(copy11x4, dim3(g), dim3(256), 0, s, (const double2 *)x, (double2 *)out, len / 4);
                     };
                     go();
                     CK(hipEventRecord(e0, s));
@@ -148,8 +162,8 @@ int main(int argc, char **argv) {
                     float ms;
                     CK(hipEventElapsedTime(&ms, e0, e1));
                     const double us = ms * 1000.0 / reps;
-                    const double b = kind == 0 ? (double)len / 4 * 32 : bytes;  // copy11 moves 16 B in + 16 B out per elem
-                    const char *nm[] = {"copy11", "copy21", "copy21u", "copy21u-nt"};
+                    const double b = (kind == 0 || kind == 4) ? (double)len / 4 * 32 : bytes;  // copy11: 16 B in + 16 B out
+                    const char *nm[] = {"copy11", "copy21", "copy21u", "copy21u-nt", "copy11x4"};
                     printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s\n", round, nm[kind], g, us, b / us / 1e3);
                 }
         }
@@ -158,12 +172,12 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[6] = {{"pf", time_variant<0>(L, s, reps)},
-                      {"nopf", time_variant<kVarNoPrefetch>(L, s, reps)},
+            } r[6] = {{"pf+ntld", time_variant<kVarNtLoad>(L, s, reps)},
                       {"nopf+ntld", time_variant<kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
-                      {"nopf+ntst", time_variant<kVarNoPrefetch | kVarNtStore>(L, s, reps)},
+                      {"nopf", time_variant<kVarNoPrefetch>(L, s, reps)},
                       {"nopf+nt2", time_variant<kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"skel", time_variant<kVarSkeleton | kVarNoPrefetch>(L, s, reps)}};
+                      {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
+                      {"skelw+pf", time_variant<kVarSkelWide | kVarNtLoad>(L, s, reps)}};
             for (auto &v : r)
                 printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s  %.3f of 8TB/s\n", round, v.name, g, v.us,
                        bytes / v.us / 1e3, bytes / v.us / 1e3 / 8000.0);
