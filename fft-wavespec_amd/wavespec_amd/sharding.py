@@ -1,0 +1,21 @@
+"""Window sharding across GPUs: contiguous window ranges,
+input slice = the range's samples plus an N - hop halo, no exchange step.
+
+The same arithmetic runs in C++ inside libmtbridge.so (batch_start in
+csrc/mtbridge.cpp) when a session spans several devices (gpu_init(-1, ...)).
+"""
+from __future__ import annotations
+
+
+def shard_windows(n_windows: int, n_shards: int, shard: int) -> tuple[int, int]:
+    """(first window, window count) of `shard`; ceil split, trailing shards may be short/empty."""
+    per = -(-n_windows // n_shards)
+    w0 = min(shard * per, n_windows)
+    return w0, max(0, min(per, n_windows - w0))
+
+
+def shard_series_slice(w0: int, nw: int, hop: int, window_len: int) -> tuple[int, int]:
+    """[start, end) of the series samples shard windows [w0, w0+nw) read (halo included)."""
+    if nw <= 0:
+        return w0 * hop, w0 * hop
+    return w0 * hop, (w0 + nw - 1) * hop + window_len
