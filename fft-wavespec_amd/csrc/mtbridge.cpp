@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -273,6 +274,11 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         K.n = c.n;
         K.f32 = c.f32;
         memcpy(K.params, kalman, sizeof(K.params));
+        static const int kvar = [] {  // tuning override: WSP_KALMAN_WPW=32|64 windows per wave
+            const char *e = getenv("WSP_KALMAN_WPW");
+            return e ? (atoi(e) == 32 ? 1 : atoi(e) == 64 ? 2 : 0) : 0;
+        }();
+        K.variant = kvar;
         HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
         L.series = d_ws;
         L.hop = c.n;

@@ -28,7 +28,10 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     a.hop = L.hop;
     a.n_windows = L.n_windows;
     a.n_groups = (L.n_windows + wpb - 1) / wpb;
-    a.vec = (L.hop % 2 == 0) && (reinterpret_cast<uintptr_t>(L.series) % (2 * sizeof(T)) == 0);
+    // pair loads (x[2n], x[2n+1]) as one 16-B (f64) / 8-B (f32) access; gfx950 under ROCm runs in
+    // unaligned-access mode, so element-aligned pairs (odd hop) are legal -- L.vec_mode 1 forces
+    // the two-scalar path for A/B
+    a.vec = L.vec_mode == 1 ? 0 : L.vec_mode == 2 ? 1 : ((L.hop % 2 == 0) && (reinterpret_cast<uintptr_t>(L.series) % (2 * sizeof(T)) == 0));
     // overlapping windows re-read samples from L2/MALL: keep them cacheable
     a.nt = L.nt_mode == 2 || (L.nt_mode == 0 && L.hop >= (int64_t(1) << L.log2n));
     window_class(L.window, &a.a0, &a.a1, &a.a2);

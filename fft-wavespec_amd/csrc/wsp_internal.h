@@ -34,6 +34,7 @@ struct SpectrumLaunch {
     double iir_apow[8];   // alpha^(32 * 2^j), j = 0..7
     int grid;             // 0 = auto
     int nt_mode;          // non-temporal sample loads: 0 = auto (hop >= N), 1 = off, 2 = on
+    int vec_mode;         // pair loads: 0 = auto (aligned only), 1 = scalar, 2 = vector even if unaligned
 };
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);
@@ -49,6 +50,7 @@ struct KalmanLaunch {
     int n;
     bool f32;
     double params[16];    // L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901 order
+    int variant;          // 0 auto, 1 = 32 windows per wave, 2 = 64 windows per wave
 };
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream);
