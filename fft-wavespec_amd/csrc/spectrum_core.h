@@ -149,7 +149,10 @@ template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int bas
 // Bartlett (evaluated exactly as L/WaveSpecZZ_1.0.2.mq5:918-922).
 enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2 };
 // Ablation bits (tools/kbench.hip only; the library uses 0).
-enum Var : int { kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32 };
+enum Var : int {
+    kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32,
+    kVarSplitLds = 64,  // real/imaginary halves exchanged separately: half the LDS, 3 waves/SIMD
+};
 
 template <typename T> struct SpecArgs {
     const T *__restrict__ series;
@@ -161,49 +164,91 @@ template <typename T> struct SpecArgs {
     // window: a0 + a1 c + a2 (2c^2 - 1); rotation by step (cs, ss) per r and
     // by (co, so) from an even to the next odd sample
     double a0, a1, a2, cs, ss, co, so, inv_theta;  // inv_theta = 2 pi/(N-1)
+    double inv_nm1;                  // 1/(N-1) for Bartlett
     double alpha, c;                 // IIR trend (L/WaveSpecZZ_1.0.2.mq5:3041-3043)
     double apow[8];                  // alpha^(32 * 2^j)
 };
 
-// Stockham pass p (0 < p < NPASS-1): LDS -> registers -> twiddle -> DFT -> LDS.
-template <typename T, int LOG2N, int PASS>
-__device__ __forceinline__ void mid_pass(cpx<T> *sl, const cpx<T> *__restrict__ tw, int t) {
+// LDS element index (padded) where pass PASS writes its element i = q*R + r.
+template <int LOG2N, int PASS> __device__ __forceinline__ int widx(int t, int i) {
     using G = Geo<LOG2N>;
-    constexpr int R = G::radix(PASS), Ns = G::ns(PASS), BPT = 16 / R;
-    constexpr int M = G::M, N = G::N, TPW = G::TPW;
-    cpx<T> v[16];
-#pragma unroll
-    for (int q = 0; q < BPT; ++q) {
-        const int b = t + TPW * q;
-        const int pb = pad16(b);
-#pragma unroll
-        for (int r = 0; r < R; ++r) v[q * R + r] = sl[pad16_at<M / R>(pb, b, r)];
-        const cpx<T> w = tw[(b % Ns) * (N / (Ns * R))];
-        cpx<T> wr = w;
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-            v[q * R + r] = cmul(v[q * R + r], wr);
-            if (r + 1 < R) wr = cmul(wr, w);
-        }
-        dft<T, R>(&v[q * R]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < BPT; ++q) {
-        const int b = t + TPW * q;
+    constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
+    const int q = i / R, r = i % R, b = t + G::TPW * q;
+    if constexpr (PASS == 0) {
+        // R consecutive elements: pad16(b R + r) = pad16(b R) + r (b R % 16 + r < 16 for R | 16)
+        return pad16(b * R) + r;
+    } else {
         const int base = (b / Ns) * Ns * R + (b % Ns);
-        const int pb = pad16(base);
-#pragma unroll
-        for (int r = 0; r < R; ++r) sl[pad16_at<Ns>(pb, base, r)] = v[q * R + r];
+        return pad16_at<Ns>(pad16(base), base, r);
     }
-    __syncthreads();
 }
 
-template <typename T, int LOG2N, int PASS>
-__device__ __forceinline__ void mid_passes(cpx<T> *sl, const cpx<T> *__restrict__ tw, int t) {
-    if constexpr (PASS < Geo<LOG2N>::NPASS - 1) {
-        mid_pass<T, LOG2N, PASS>(sl, tw, t);
-        mid_passes<T, LOG2N, PASS + 1>(sl, tw, t);
+// LDS element index pass PASS reads its element i from (the final pass owns
+// butterflies {t, B-t}, {0, B/2} for t = 0).
+template <int LOG2N, int PASS> __device__ __forceinline__ int ridx(int t, int i) {
+    using G = Geo<LOG2N>;
+    if constexpr (PASS == G::NPASS - 1) {
+        const int q = i / 8, r = i % 8;
+        const int b = q == 0 ? t : (t == 0 ? G::TPW : 2 * G::TPW - t);
+        return pad16_at<G::B>(pad16(b), b, r);
+    } else {
+        constexpr int R = G::radix(PASS);
+        const int q = i / R, r = i % R, b = t + G::TPW * q;
+        return pad16_at<G::M / R>(pad16(b), b, r);
+    }
+}
+
+// LDS transpose between passes: write v at widx<PASS>, read v at ridx<PASS+1>.
+// AoS: one complex per ds_write_b128/ds_read_b128 (f64), 2 barriers.  SPLIT:
+// real parts then imaginary parts through half the LDS, 4 barriers.
+template <bool SPLIT, typename T, int LOG2N, int PASS>
+__device__ __forceinline__ void exchange(char *base, cpx<T> (&v)[16], int t) {
+    if constexpr (!SPLIT) {
+        cpx<T> *s = reinterpret_cast<cpx<T> *>(base);
+        __syncthreads();  // every read of the previous contents is done
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = s[ridx<LOG2N, PASS + 1>(t, i)];
+    } else {
+        T *s = reinterpret_cast<T *>(base);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].re;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i].re = s[ridx<LOG2N, PASS + 1>(t, i)];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].im;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i].im = s[ridx<LOG2N, PASS + 1>(t, i)];
+    }
+}
+
+// Stockham pass 0 < PASS < NPASS-1 on data already in its read layout:
+// twiddle W^(r (b mod Ns)) then in-register radix-R DFTs, then the exchange.
+template <bool SPLIT, typename T, int LOG2N, int PASS>
+__device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cpx<T> *__restrict__ tw, int t) {
+    using G = Geo<LOG2N>;
+    if constexpr (PASS < G::NPASS - 1) {
+        constexpr int R = G::radix(PASS), Ns = G::ns(PASS), BPT = 16 / R;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int b = t + G::TPW * q;
+            const cpx<T> w = tw[(b % Ns) * (G::N / (Ns * R))];
+            cpx<T> wr = w;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                v[q * R + r] = cmul(v[q * R + r], wr);
+                if (r + 1 < R) wr = cmul(wr, w);
+            }
+            dft<T, R>(&v[q * R]);
+        }
+        exchange<SPLIT, T, LOG2N, PASS>(base, v, t);
+        mid_passes<SPLIT, T, LOG2N, PASS + 1>(base, v, tw, t);
     }
 }
 
@@ -239,13 +284,14 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
-__global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
+__global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? 3 : 2) void spectrum_kernel(SpecArgs<T> a) {
     using G = Geo<LOG2N>;
     using v2 = typename V2<T>::t;
     constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B;
     constexpr int R0 = G::R0, BPT0 = G::BPT0;
     constexpr bool kPrefetch = !(VAR & kVarNoPrefetch);
-    constexpr int kCplx = WPB * SLOT * (int)sizeof(cpx<T>);
+    constexpr bool kSplit = VAR & kVarSplitLds;
+    constexpr int kCplx = WPB * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));
     constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
     constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
     constexpr int kScan = 16 * 8;
@@ -255,7 +301,7 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
     const int tid = threadIdx.x;
     const int slot = tid / TPW;
     const int t = tid % TPW;
-    cpx<T> *sl = reinterpret_cast<cpx<T> *>(smem) + slot * SLOT;
+    char *lbase = smem + slot * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));  // this window's LDS slot
 
     // per-thread window rotation start: th_i at i = 2 (t + TPW q)
     double wc0[BPT0], ws0[BPT0];
@@ -394,9 +440,11 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
                     s = s * a.cs + c * a.ss;
                     c = cn;
                 } else if constexpr (WCLASS == kWinBartlett) {
-                    const int i = 2 * ((t + TPW * q) + (M / R0) * r);
-                    da *= 1.0 - fabs((2.0 * i - N + 1) / (N - 1));
-                    db *= 1.0 - fabs((2.0 * (i + 1) - N + 1) / (N - 1));
+                    int tq = t + TPW * q;
+                    asm volatile("" : "+v"(tq));  // recompute per window: no hoisted 32-value table
+                    const int i = 2 * (tq + (M / R0) * r);
+                    da *= 1.0 - fabs((2.0 * i - N + 1) * a.inv_nm1);
+                    db *= 1.0 - fabs((2.0 * (i + 1) - N + 1) * a.inv_nm1);
                 }
                 v[q * R0 + r] = {T(da), T(db)};
             }
@@ -431,29 +479,16 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
 
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) dft<T, R0>(&v[q * R0]);
-        __syncthreads();  // previous group's final-pass LDS reads are done
-#pragma unroll
-        for (int q = 0; q < BPT0; ++q) {
-            const int b = t + TPW * q;
-            // R0 consecutive elements: pad16(b R0 + r) = pad16(b R0) + r when
-            // b R0 % 16 + r < 16 (always for R0 = 16; r < R0 divides 16)
-            const int pb = pad16(b * R0);
-#pragma unroll
-            for (int r = 0; r < R0; ++r) sl[pb + r] = v[q * R0 + r];
-        }
-        __syncthreads();
-
-        // ---- middle passes
-        mid_passes<T, LOG2N, 1>(sl, a.tw, t);
+        exchange<kSplit, T, LOG2N, 0>(lbase, v, t);  // also orders the previous group's reads
+        mid_passes<kSplit, T, LOG2N, 1>(lbase, v, a.tw, t);
 
         // ---- final radix-8 pass: thread t owns butterflies {t, B-t} ({0, B/2} for t = 0)
         const int bq0 = t, bq1 = t == 0 ? TPW : 2 * TPW - t;
         cpx<T> u0[8], u1[8];
-        const int pq0 = pad16(bq0), pq1 = pad16(bq1);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            u0[r] = sl[pad16_at<B>(pq0, bq0, r)];
-            u1[r] = sl[pad16_at<B>(pq1, bq1, r)];
+            u0[r] = v[r];
+            u1[r] = v[8 + r];
         }
         if constexpr (G::NPASS > 1) {
             const cpx<T> w0 = a.tw[2 * bq0], w1 = a.tw[2 * bq1];  // (b % Ns) * N/(Ns*8) with Ns = B
@@ -498,7 +533,7 @@ __global__ __launch_bounds__(kBlock, 2) void spectrum_kernel(SpecArgs<T> a) {
         const cpx<T> wt = a.tw[t];
         const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
-        T *prow = reinterpret_cast<T *>(sl);  // power row staged in this window's LDS slot
+        T *prow = reinterpret_cast<T *>(lbase);  // power row staged in this window's LDS slot
         if constexpr (OUT == kOutPower) __syncthreads();  // every final-pass LDS read is done
 #pragma unroll
         for (int s = 0; s < 8; ++s) {

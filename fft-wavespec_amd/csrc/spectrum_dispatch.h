@@ -43,6 +43,7 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     const long double two_pi = 6.283185307179586476925286766559005768L;
     const long double th = two_pi / (long double)(n - 1);
     a.inv_theta = (double)th;
+    a.inv_nm1 = 1.0 / (double)(n - 1);
     a.cs = (double)cosl(th * (long double)(2 * (m / r0)));
     a.ss = (double)sinl(th * (long double)(2 * (m / r0)));
     a.co = (double)cosl(th);
@@ -53,14 +54,23 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     return a;
 }
 
-// Library default (profiles/r01/kbench_*.log, interleaved rounds): no register
-// prefetch (slower at the LDS-limited 2 waves/SIMD), non-temporal 16-B stores
-// of the LDS-staged power row, a 16384-workgroup grid-stride launch.  The
-// sample loads are non-temporal only when windows do not overlap (a.nt).
-constexpr int kDefaultVar = kVarNoPrefetch | kVarNtStore;
-constexpr int kDefaultGrid = 16384;
+// Library default (profiles/r01/kbench_*.log, interleaved rounds): real/imag
+// split LDS exchange (17.5 KiB, 3 waves/SIMD -> 6 workgroups/CU), no register
+// prefetch, non-temporal 16-B stores of the LDS-staged power row, 32768
+// workgroups grid-striding.  Sample loads are non-temporal only when windows
+// do not overlap (a.nt).  The IIR path (33 KiB detrend staging caps it at 4
+// workgroups/CU anyway) and the packed output (spills at 168 VGPRs) keep the
+// AoS exchange at 2 waves/SIMD.
+constexpr int kDefaultVar = kVarNoPrefetch | kVarNtStore | kVarSplitLds;
+constexpr int kDefaultGrid = 32768;
+template <typename T, int DETREND, int OUT> constexpr int default_var() {
+    // the f32 mean path converts every sample to fp64 for the reduction and spills at 168
+    return (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean))
+               ? (kVarNoPrefetch | kVarNtStore)
+               : kDefaultVar;
+}
 
-template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = kDefaultVar>
+template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, DETREND, OUT>()>
 hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
     using G = Geo<LOG2N>;
     const SpecArgs<T> a = make_args<T>(L, G::WPB);

@@ -182,7 +182,7 @@ int main(int argc, char **argv) {
     printf("# W=%lld N=%d algorithmic bytes=%.3f GB, roofline(8 TB/s)=%.1f us\n", (long long)W, n, bytes / 1e9,
            bytes / 8e12 * 1e6);
 
-    const int grids[] = {1024, 4096, 8192, 16384, 32768, 65536};
+    const int grids[] = {4096, 8192, 16384, 32768, 65536};
     for (int round = 0; round < rounds; ++round) {
         // copy ceiling
         {
@@ -221,10 +221,10 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[6] = {{"pf+ntld", time_variant<kVarNtLoad>(L, s, reps)},
-                      {"nopf+ntld", time_variant<kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
-                      {"nopf", time_variant<kVarNoPrefetch>(L, s, reps)},
-                      {"nopf+nt2", time_variant<kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+            } r[6] = {{"nopf+nt2", time_variant<kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+ntld", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
+                      {"pf+nt2", time_variant<kVarNtLoad | kVarNtStore>(L, s, reps)},
                       {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
                       {"skelw+pf", time_variant<kVarSkelWide | kVarNtLoad>(L, s, reps)}};
             for (auto &v : r)

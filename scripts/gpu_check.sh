@@ -10,7 +10,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_
 rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-if [ -x fft-wavespec_amd/bin/kbench ]; then
+if [ -x fft-wavespec_amd/bin/kbench ] && [ "${KBENCH:-0}" = 1 ]; then
   timeout -k 10 300 fft-wavespec_amd/bin/kbench 65536 20 2 > gpurun_out/kbench_$TAG.log 2>&1
   rc=$?; echo "kbench rc=$rc"; cat gpurun_out/kbench_$TAG.log
   [ $rc -eq 0 ] || exit $rc
