@@ -152,6 +152,7 @@ enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2 };
 enum Var : int {
     kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32,
     kVarSplitLds = 64,  // real/imaginary halves exchanged separately: half the LDS, 3 waves/SIMD
+    kVarOcc4 = 128,     // with kVarSplitLds: 4 waves/SIMD (8 workgroups/CU, <= 128 VGPRs)
 };
 
 template <typename T> struct SpecArgs {
@@ -284,7 +285,7 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
-__global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? 3 : 2) void spectrum_kernel(SpecArgs<T> a) {
+__global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
     using G = Geo<LOG2N>;
     using v2 = typename V2<T>::t;
     constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B;

@@ -182,10 +182,10 @@ int main(int argc, char **argv) {
     printf("# W=%lld N=%d algorithmic bytes=%.3f GB, roofline(8 TB/s)=%.1f us\n", (long long)W, n, bytes / 1e9,
            bytes / 8e12 * 1e6);
 
-    const int grids[] = {4096, 8192, 16384, 32768, 65536};
+    const int grids[] = {8192, 16384, 32768, 65536};
     for (int round = 0; round < rounds; ++round) {
         // copy ceiling
-        {
+        if (getenv("KBENCH_COPIES")) {
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0));
             CK(hipEventCreate(&e1));
@@ -221,12 +221,10 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[6] = {{"nopf+nt2", time_variant<kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"split+ntld", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
-                      {"pf+nt2", time_variant<kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)},
-                      {"skelw+pf", time_variant<kVarSkelWide | kVarNtLoad>(L, s, reps)}};
+            } r[4] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+occ4+nt2", time_variant<kVarSplitLds | kVarOcc4 | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+blk+nt2", time_variant<kVarSplitLds | kVarBlocked | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)}};
             for (auto &v : r)
                 printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s  %.3f of 8TB/s\n", round, v.name, g, v.us,
                        bytes / v.us / 1e3, bytes / v.us / 1e3 / 8000.0);

@@ -5,8 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1
-for CFG in c2 c3 c4 north_star; do
-  timeout -k 10 400 python bench.py --config $CFG --steps 20 --warmup 3 --cpu-seconds 5 > gpurun_out/bench_${TAG}_$CFG.json 2> gpurun_out/bench_${TAG}_$CFG.err
+for CFG in c2 c3 c4 c5 north_star; do
+  timeout -k 10 400 python bench.py --config $CFG --cpu-seconds 5 > gpurun_out/bench_${TAG}_$CFG.json 2> gpurun_out/bench_${TAG}_$CFG.err
   rc=$?; echo "$CFG rc=$rc"; cat gpurun_out/bench_${TAG}_$CFG.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_${TAG}_$CFG.err; exit $rc; }
 done
 for CFG in c2 c3 c4; do
