@@ -205,9 +205,10 @@ struct Config {
     int n = 0, log2n = 0;
     int64_t hop = 0, n_windows = 0;
     int detrend = 0, window = 0, trend_period = 0, output = 0;
+    int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
-    int64_t record() const { return output == MTB_OUT_PACKED ? n : n / 2; }
+    int64_t record() const { return output == MTB_OUT_PACKED ? n : output == MTB_OUT_TOPK ? 4 * topk : n / 2; }
     int64_t series_elems() const { return (n_windows - 1) * hop + n; }
     int64_t unique_input_elems() const { return hop >= n ? n_windows * (int64_t)n : series_elems(); }
 };
@@ -218,6 +219,8 @@ int ilog2_exact(int n) {
     while ((1 << l) < n) ++l;
     return l;
 }
+
+int config_set_topk(Config *c, int top_k, double min_period, double max_period);
 
 int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int window, int trend_period,
                 int precision, int output, Config *c) {
@@ -232,7 +235,7 @@ int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int
     }
     if (detrend < MTB_DETREND_NONE || detrend > MTB_DETREND_KALMAN || window < MTB_WINDOW_NONE ||
         window > MTB_WINDOW_BARTLETT || (precision != MTB_PREC_F64 && precision != MTB_PREC_F32) ||
-        (output != MTB_OUT_POWER && output != MTB_OUT_PACKED)) {
+        (output != MTB_OUT_POWER && output != MTB_OUT_PACKED && output != MTB_OUT_TOPK)) {
         set_error("bad mode: detrend=%d window=%d precision=%d output=%d", detrend, window, precision, output);
         return MTB_BAD_ARGS;
     }
@@ -246,6 +249,25 @@ int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int
     c->trend_period = trend_period;
     c->output = output;
     c->f32 = precision == MTB_PREC_F32;
+    // MTB_OUT_TOPK through the generic entry points: the reference's own scan
+    // parameters (top 8, InpMinPeriod 18 / InpMaxPeriod 200, 1.1.0:22-23)
+    if (output == MTB_OUT_TOPK) return config_set_topk(c, 8, 18.0, 200.0);
+    return MTB_OK;
+}
+
+// Top-k range of L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:539-541.
+int config_set_topk(Config *c, int top_k, double min_period, double max_period) {
+    if (top_k < 1 || top_k > 64 || !(min_period > 0.0) || !(max_period > 0.0)) {
+        set_error("top_k=%d min_period=%g max_period=%g: need 1 <= top_k <= 64 and positive periods", top_k,
+                  min_period, max_period);
+        return MTB_BAD_ARGS;
+    }
+    c->output = MTB_OUT_TOPK;
+    c->topk = top_k;
+    c->kmin = (int)ceil((double)c->n / max_period);
+    c->kmax = (int)floor((double)c->n / min_period);
+    if (c->kmax >= c->n / 2) c->kmax = c->n / 2 - 1;
+    if (c->kmin < 0) c->kmin = 0;
     return MTB_OK;
 }
 
@@ -291,6 +313,9 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
     L.log2n = c.log2n;
     L.output = c.output;
     L.f32 = c.f32;
+    L.topk = c.topk;
+    L.kmin = c.kmin;
+    L.kmax = c.kmax;
     if (L.detrend == kDetrendIir) {
         // L/WaveSpecZZ_1.0.2.mq5:3041-3043, same double expressions as the CPU path
         const double omega = 2.0 * M_PI / c.trend_period;
@@ -597,6 +622,25 @@ MTB_API int32_t gpu_spectrum_batch(const double *series, int32_t series_len, int
     return run_sync(c, series, out, out_cap, out_len);
 }
 
+MTB_API int32_t gpu_spectrum_topk_batch(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
+                                        int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
+                                        int32_t top_k, double min_period, double max_period, double *out,
+                                        int32_t out_cap, int32_t *out_len) {
+    if (out_len) *out_len = 0;
+    Config c;
+    int st = spectrum_config(series, series_len, window_len, hop, detrend, window, trend_period, precision,
+                             MTB_OUT_POWER, &c);
+    if (st != MTB_OK) return st;
+    st = config_set_topk(&c, top_k, min_period, max_period);
+    if (st != MTB_OK) return st;
+    if (!out || out_cap < c.record()) {
+        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)c.record());
+        return MTB_BAD_ARGS;
+    }
+    c.n_windows = std::min<int64_t>(c.n_windows, out_cap / c.record());
+    return run_sync(c, series, out, out_cap, out_len);
+}
+
 MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_len, int32_t window_len,
                                           int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
                                           int32_t precision, int32_t output, int64_t *job_id) {
@@ -765,6 +809,16 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
         return MTB_BAD_ARGS;
     }
     return enqueue(p->dev, p->cfg, p->kalman, d_series, d_out, p->d_ws, (hipStream_t)hip_stream);
+}
+
+MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period) {
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    auto it = g_plans->find(plan);
+    if (it == g_plans->end()) {
+        set_error("unknown plan %lld", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    return config_set_topk(&it->second->cfg, top_k, min_period, max_period);
 }
 
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan) {

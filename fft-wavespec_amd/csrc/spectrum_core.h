@@ -166,6 +166,7 @@ template <typename T> struct SpecArgs {
     // by (co, so) from an even to the next odd sample
     double a0, a1, a2, cs, ss, co, so, inv_theta;  // inv_theta = 2 pi/(N-1)
     double inv_nm1;                  // 1/(N-1) for Bartlett
+    int topk, kmin, kmax;            // kOutTopK: k slots over bins [kmin, kmax]
     double alpha, c;                 // IIR trend (L/WaveSpecZZ_1.0.2.mq5:3041-3043)
     double apow[8];                  // alpha^(32 * 2^j)
 };
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
         const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
         T *prow = reinterpret_cast<T *>(lbase);  // power row staged in this window's LDS slot
-        if constexpr (OUT == kOutPower) __syncthreads();  // every final-pass LDS read is done
+        if constexpr (OUT != kOutPacked) __syncthreads();  // every final-pass LDS read is done
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const cpx<T> A = u0[s], Bv = u1[7 - s];
@@ -557,6 +558,10 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
             if constexpr (OUT == kOutPower) {
                 prow[ka] = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
                 prow[kb] = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+            } else if constexpr (OUT == kOutTopK) {  // stage X for the scan (AoS slot)
+                cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
+                xrow[ka] = {T(0.5) * xa.re, T(0.5) * xa.im};
+                xrow[kb] = {T(0.5) * xb.re, T(0.5) * xb.im};
             } else if (active) {  // packed: (Re, Im) of one bin is already one 16-B (8-B) store
                 v2 oa, ob;
                 oa.x = T(0.5) * xa.re;
@@ -565,6 +570,69 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
                 ob.y = T(0.5) * xb.im;
                 *reinterpret_cast<v2 *>(a.out + w * N + 2 * ka) = oa;
                 *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
+            }
+        }
+        if constexpr (OUT == kOutTopK) {
+            // Top-k bin scan (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554):
+            // k rounds of argmax over bins [kmin, kmax] ordered (power desc, bin asc) -- the
+            // order the reference's strict-'>' insertion in ascending bin order produces.  The
+            // winner's owner writes [bin, power, Re X, Im X] and retires the bin (NaN power).
+            cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
+            constexpr int SW = TPW < 64 ? TPW : 64;
+            constexpr int kNone = 0x7fffffff;
+            __syncthreads();  // X row complete
+            for (int s = 0; s < a.topk; ++s) {
+                T bp = T(-1);
+                int bb = kNone;
+                for (int b = a.kmin + t; b <= a.kmax; b += TPW) {
+                    const cpx<T> x = xrow[b];
+                    const T p = x.re * x.re + x.im * x.im;
+                    if (p > bp || (p == bp && b < bb)) {
+                        bp = p;
+                        bb = b;
+                    }
+                }
+#pragma unroll
+                for (int off = SW / 2; off >= 1; off >>= 1) {
+                    const T op = __shfl_xor(bp, off, SW);
+                    const int ob = __shfl_xor(bb, off, SW);
+                    if (op > bp || (op == bp && ob < bb)) {
+                        bp = op;
+                        bb = ob;
+                    }
+                }
+                if constexpr (TPW == 128) {
+                    int *sb = reinterpret_cast<int *>(scanbuf + 2);
+                    if ((tid & 63) == 0) {
+                        scanbuf[tid >> 6] = (double)bp;
+                        sb[tid >> 6] = bb;
+                    }
+                    __syncthreads();
+                    const T p0 = (T)scanbuf[0], p1 = (T)scanbuf[1];
+                    const int b0 = sb[0], b1 = sb[1];
+                    const bool second = p1 > p0 || (p1 == p0 && b1 < b0);
+                    bp = second ? p1 : p0;
+                    bb = second ? b1 : b0;
+                }
+                T *rec = a.out + w * (int64_t)(4 * a.topk) + 4 * s;
+                if (bb != kNone) {
+                    if ((bb - a.kmin) % TPW == t) {
+                        const cpx<T> x = xrow[bb];
+                        if (active) {
+                            rec[0] = T(bb);
+                            rec[1] = bp;
+                            rec[2] = x.re;
+                            rec[3] = x.im;
+                        }
+                        xrow[bb] = {T(__builtin_nan("")), T(__builtin_nan(""))};
+                    }
+                } else if (t == 0 && active) {  // fewer than k bins in range: (-1, -1) slots
+                    rec[0] = T(-1);
+                    rec[1] = T(-1);
+                    rec[2] = T(0);
+                    rec[3] = T(0);
+                }
+                if constexpr (TPW == 128) __syncthreads();  // retirement visible to both waves
             }
         }
         if constexpr (OUT == kOutPower) {

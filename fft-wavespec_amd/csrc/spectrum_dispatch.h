@@ -48,6 +48,9 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     a.ss = (double)sinl(th * (long double)(2 * (m / r0)));
     a.co = (double)cosl(th);
     a.so = (double)sinl(th);
+    a.topk = L.topk;
+    a.kmin = L.kmin;
+    a.kmax = L.kmax;
     a.alpha = L.iir_alpha;
     a.c = L.iir_c;
     for (int j = 0; j < 8; ++j) a.apow[j] = L.iir_apow[j];
@@ -94,8 +97,11 @@ hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
 
 template <typename T, int LOG2N, int DETREND>
 hipError_t dispatch_out(const SpectrumLaunch &L, hipStream_t s) {
-    return L.output == kOutPacked ? dispatch_win<T, LOG2N, DETREND, kOutPacked>(L, s)
-                                  : dispatch_win<T, LOG2N, DETREND, kOutPower>(L, s);
+    switch (L.output) {
+    case kOutPacked: return dispatch_win<T, LOG2N, DETREND, kOutPacked>(L, s);
+    case kOutTopK: return dispatch_win<T, LOG2N, DETREND, kOutTopK>(L, s);
+    default: return dispatch_win<T, LOG2N, DETREND, kOutPower>(L, s);
+    }
 }
 
 template <typename T, int LOG2N> hipError_t dispatch_detrend(const SpectrumLaunch &L, hipStream_t s) {

@@ -14,7 +14,7 @@ constexpr int kMaxLog2N = 12;  // N = 4096
 constexpr int kBlock = 128;    // threads per workgroup (2 waves)
 
 enum Detrend : int { kDetrendNone = 0, kDetrendMean = 1, kDetrendIir = 2, kDetrendKalman = 3 };
-enum Output : int { kOutPower = 0, kOutPacked = 1 };
+enum Output : int { kOutPower = 0, kOutPacked = 1, kOutTopK = 2 };
 
 // Everything a spectrum launch needs; pointer types are erased so one
 // struct serves the f64 and f32 instantiations.
@@ -29,6 +29,8 @@ struct SpectrumLaunch {
     int detrend;          // kDetrendNone/Mean/Iir (Kalman runs as a pre-pass)
     int output;
     bool f32;
+    // top-k scan (kOutTopK): k slots, bins [kmin, kmax] (gpuopt-nodetrend.mq5:536-554)
+    int topk, kmin, kmax;
     // IIR trend coefficients (L/WaveSpecZZ_1.0.2.mq5:3041-3043), always fp64
     double iir_alpha, iir_c;
     double iir_apow[8];   // alpha^(32 * 2^j), j = 0..7

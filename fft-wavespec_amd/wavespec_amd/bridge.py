@@ -24,7 +24,7 @@ STATUS_NAMES = {OK: "OK", BAD_ARGS: "BAD_ARGS", BACKEND_UNAVAILABLE: "BACKEND_UN
 DETREND = {"none": 0, "mean": 1, "iir": 2, "kalman": 3}
 WINDOW = {"none": 0, "hann": 1, "hamming": 2, "blackman": 3, "bartlett": 4}
 PRECISION = {"f64": 0, "f32": 1}
-OUTPUT = {"power": 0, "packed": 1}
+OUTPUT = {"power": 0, "packed": 1, "topk": 2}
 
 _d = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)
@@ -52,6 +52,9 @@ SIGNATURES = {
                                               C.c_int32, C.c_int32, C.c_int32, _i64p]),
     "gpu_try_get_spectrum_batch": (C.c_int32, [C.c_int64, _d, C.c_int32, _i32p, _i32p]),
     "gpu_set_kalman_params": (C.c_int32, [_d, C.c_int32]),
+    "gpu_spectrum_topk_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                            C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32, _i32p]),
+    "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_execute": (C.c_int32, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -145,6 +148,21 @@ def spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none"
     return out[: n_out.value]
 
 
+def spectrum_topk_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
+                        trend_period: int = 0, precision="f64", top_k: int = 8, min_period: float = 18.0,
+                        max_period: float = 200.0) -> np.ndarray:
+    """gpu_spectrum_topk_batch -> (nwin, top_k, 4) records [bin, power, Re X, Im X]."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - window_len) // hop
+    out = np.empty((nwin, top_k, 4), dtype=np.float64)
+    n_out = C.c_int32(0)
+    _check("gpu_spectrum_topk_batch",
+           lib().gpu_spectrum_topk_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
+                                         trend_period, PRECISION[precision], top_k, min_period, max_period,
+                                         _dptr(out), out.size, C.byref(n_out)))
+    return out[: n_out.value]
+
+
 def submit_spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
                           trend_period: int = 0, precision="f64", output="power") -> int:
     s = np.ascontiguousarray(series, dtype=np.float64)
@@ -184,6 +202,10 @@ class Plan:
         self.window_len, self.hop, self.n_windows = window_len, hop, n_windows
         self.record = window_len if OUTPUT[output] == 1 else window_len // 2
         self.series_len = (n_windows - 1) * hop + window_len
+
+    def set_topk(self, top_k: int, min_period: float, max_period: float) -> None:
+        _check("wsp_plan_set_topk", lib().wsp_plan_set_topk(self.handle, top_k, min_period, max_period))
+        self.record = 4 * top_k
 
     @property
     def algorithmic_bytes(self) -> int:

@@ -56,6 +56,11 @@ extern "C" {
  * (1.1.0:522-528). */
 #define MTB_OUT_POWER 0
 #define MTB_OUT_PACKED 1
+/* top-k bin scan records (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554):
+ * top_k slots of [bin, power, Re X_bin, Im X_bin], power-descending (ties: lower bin first),
+ * bins in [ceil(N/max_period), floor(N/min_period)] clamped to N/2-1, empty slots
+ * [-1, -1, 0, 0]. */
+#define MTB_OUT_TOPK 2
 
 /* =====================================================================
  * 1. Reference surface -- Include/imports.mqh:5-19 (exact signatures)
@@ -146,6 +151,14 @@ MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_l
 MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t out_cap, int32_t *out_len,
                                            int32_t *ready);
 
+/* The spectrum's immediate consumer fused into the same launch: only
+ * 4*top_k doubles per window leave the device instead of N/2 (MTB_OUT_TOPK
+ * record layout).  top_k in 1..64 (the reference uses 8); periods in bars. */
+MTB_API int32_t gpu_spectrum_topk_batch(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
+                                        int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
+                                        int32_t top_k, double min_period, double max_period, double *out,
+                                        int32_t out_cap, int32_t *out_len);
+
 /* Kalman 4D parameters for MTB_DETREND_KALMAN, in the order of the inputs
  * at L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901: follow_strength,
  * q_pos, q_vel, q_acc, q_jerk, adapt_gain, meas_noise, init_var_pos,
@@ -170,6 +183,9 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
  * precision, >= (n_windows-1)*hop + window_len elements) and writing d_out
  * (n_windows * record elements).  Asynchronous; no allocation, no sync. */
 MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream);
+
+/* Switches a plan to MTB_OUT_TOPK records (4*top_k elements per window). */
+MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period);
 
 /* Bytes the plan's algorithm must move per execute: unique input samples
  * + output, for roofline accounting. */

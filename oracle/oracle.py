@@ -47,6 +47,10 @@ def lib() -> C.CDLL:
         h.ora_detrend_mean.argtypes = [_d, C.c_int, _d]
         h.ora_kalman_trend.argtypes = [_d, C.c_int, _d, _d]
         h.ora_gather_series.argtypes = [_d, C.c_int64, C.c_int, _d]
+        h.ora_topk_bins.argtypes = [_d, _d, C.c_int, C.c_int, C.c_double, C.c_double, _d]
+        h.ora_batch_topk.argtypes = [_d, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, _d, C.c_int,
+                                     C.c_double, C.c_double, _d]
+        h.ora_batch_topk.restype = C.c_int64
         _lib = h
     return _lib
 
@@ -88,6 +92,19 @@ def batch_spectrum(series, n, hop, detrend="none", window="hann", trend_period=0
     got = lib().ora_batch_spectrum(_p(s), s.size, n, hop, nwin, DETREND[detrend], WINDOW[window], trend_period,
                                    None if kp is None else _p(kp), 1 if output == "packed" else 0, _p(out))
     assert got == nwin, (got, nwin)
+    return out
+
+
+def batch_topk(series, n, hop, detrend="none", window="hann", trend_period=0, kalman=None, top_k=8,
+               min_period=18.0, max_period=200.0) -> np.ndarray:
+    """(nwin, top_k, 4) records [bin, power, Re X, Im X] (gpuopt-nodetrend.mq5:536-554)."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - n) // hop
+    out = np.empty((nwin, top_k, 4))
+    kp = np.ascontiguousarray(KALMAN_DEFAULTS if kalman is None else kalman, dtype=np.float64)
+    got = lib().ora_batch_topk(_p(s), s.size, n, hop, DETREND[detrend], WINDOW[window], trend_period, _p(kp), top_k,
+                               min_period, max_period, _p(out))
+    assert got == nwin
     return out
 
 

@@ -310,6 +310,43 @@ ORA_EXPORT void ora_power(const double *re, const double *im, int n, double *spe
     for (int k = 0; k < n / 2; k++) spec[k] = re[k] * re[k] + im[k] * im[k];
 }
 
+/* ------------------------------------------------------------- top-k scan */
+
+/* Top-k bin scan of L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554
+ * (the immediate consumer of the spectrum in the 1.1.0 predecessor), with k
+ * generalised from 8: bins in [ceil(N/MaxP), floor(N/MinP)] (max clamped to
+ * bins-1), inserted in ascending bin order with a strict '>' (ties keep the
+ * earlier bin), empty slots (-1, -1).  Record per slot: bin, power, Re X,
+ * Im X (phase/amplitude reconstruction :559-573 needs Re/Im). */
+ORA_EXPORT void ora_topk_bins(const double *re, const double *im, int n, int top_k, double min_period,
+                              double max_period, double *rec) {
+    double top_pow[64];
+    int top_bin[64];
+    if (top_k > 64) top_k = 64;
+    for (int s = 0; s < top_k; s++) { top_pow[s] = -1.0; top_bin[s] = -1; }
+    const int bins = n / 2;
+    int min_index = (int)ceil((double)n / max_period);
+    int max_index = (int)floor((double)n / min_period);
+    if (max_index >= bins) max_index = bins - 1;
+    for (int b = min_index; b <= max_index; b++) {
+        if (b < 0) continue;
+        double p = re[b] * re[b] + im[b] * im[b];
+        for (int s = 0; s < top_k; s++) {
+            if (p > top_pow[s]) {
+                for (int t = top_k - 1; t > s; t--) { top_pow[t] = top_pow[t - 1]; top_bin[t] = top_bin[t - 1]; }
+                top_pow[s] = p; top_bin[s] = b;
+                break;
+            }
+        }
+    }
+    for (int s = 0; s < top_k; s++) {
+        rec[4 * s] = top_bin[s];
+        rec[4 * s + 1] = top_pow[s];
+        rec[4 * s + 2] = top_bin[s] >= 0 ? re[top_bin[s]] : 0.0;
+        rec[4 * s + 3] = top_bin[s] >= 0 ? im[top_bin[s]] : 0.0;
+    }
+}
+
 /* ---------------------------------------------------------- full pipeline */
 
 static int is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
@@ -340,6 +377,25 @@ ORA_EXPORT int ora_window_spectrum(const double *x, int n, int detrend, int wind
     else ora_power(re, im, n, out);
     free(d); free(re); free(im);
     return 0;
+}
+
+/* Top-k records for every window of a series (4*top_k doubles per window). */
+ORA_EXPORT int64_t ora_batch_topk(const double *series, int64_t series_len, int n, int64_t hop, int detrend,
+                                  int window, int trend_period, const double *kalman16, int top_k, double min_period,
+                                  double max_period, double *out) {
+    if (!is_pow2(n) || hop <= 0 || series_len < n) return -1;
+    int64_t nwin = 1 + (series_len - n) / hop;
+#pragma omp parallel for schedule(static)
+    for (int64_t w = 0; w < nwin; w++) {
+        double *packed = (double *)malloc(sizeof(double) * (size_t)n);
+        double *re = (double *)malloc(sizeof(double) * (size_t)n / 2);
+        double *im = (double *)malloc(sizeof(double) * (size_t)n / 2);
+        ora_window_spectrum(series + w * hop, n, detrend, window, trend_period, kalman16, 1, packed);
+        for (int k = 0; k < n / 2; k++) { re[k] = packed[2 * k]; im[k] = packed[2 * k + 1]; }
+        ora_topk_bins(re, im, n, top_k, min_period, max_period, out + w * 4 * top_k);
+        free(packed); free(re); free(im);
+    }
+    return nwin;
 }
 
 /* Batch over a chronological series: window w = series[w*hop, w*hop+N).

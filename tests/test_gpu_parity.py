@@ -234,3 +234,47 @@ def test_golden_vectors_on_gpu(gpu_session, path):
     g = np.load(path, allow_pickle=False)
     p = gpu(g["series"], int(g["n"]), int(g["hop"]), str(g["detrend"]), str(g["window"]), int(g["trend_period"]))
     assert oracle.rel_err(p, g["power"]) <= 1e-10
+
+
+def _topk_match(got, want, tol):
+    """Bins identical except where two candidates' powers tie within tol (the order of a near-tie
+    is decided by rounding); powers and Re/Im within tol of the oracle's."""
+    assert got.shape == want.shape
+    for w in range(got.shape[0]):
+        gb, wb = got[w, :, 0].astype(int), want[w, :, 0].astype(int)
+        scale = max(want[w, 0, 1], 1e-300)
+        for s in np.nonzero(gb != wb)[0]:
+            assert abs(got[w, s, 1] - want[w, s, 1]) <= tol * scale, (w, s, gb, wb)
+        assert np.max(np.abs(got[w, :, 1] - want[w, :, 1])) <= tol * scale
+        amp = max(np.sqrt(scale), 1e-300)
+        same = gb == wb
+        assert np.max(np.abs(got[w, same, 2:] - want[w, same, 2:]), initial=0.0) <= tol * amp * 10
+
+
+@pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),
+                                               (256, 256, 16, 2, 10000), (512, 512, 8, 300, 400)])
+@pytest.mark.parametrize("detrend", ["none", "iir"])
+def test_topk_scan(gpu_session, n, hop, k, minp, maxp, detrend):
+    """Fused top-k bin scan (gpuopt-nodetrend.mq5:536-554) against the oracle."""
+    s = synth.random_walk((40 - 1) * hop + n, seed=n + k)
+    got = bridge.spectrum_topk_batch(s, n, hop, detrend, "hann", 1024, "f64", k, minp, maxp)
+    want = oracle.batch_topk(s, n, hop, detrend, "hann", 1024, None, k, minp, maxp)
+    _topk_match(got, want, 1e-10)
+
+
+def test_topk_f32_and_plan(gpu_session):
+    torch = pytest.importorskip("torch")
+    n, w = 2048, 300
+    s = synth.random_walk(n * w, seed=3)
+    got = bridge.spectrum_topk_batch(s, n, n, "none", "hann", 0, "f32", 8, 18, 200)
+    want = oracle.batch_topk(s.astype(np.float32).astype(np.float64), n, n, "none", "hann", 0, None, 8, 18, 200)
+    _topk_match(got, want, 1e-5)
+    plan = bridge.Plan(0, n, n, w, "none", "hann")
+    plan.set_topk(8, 18, 200)
+    d_s = torch.from_numpy(s).cuda()
+    d_o = torch.empty(w * 32, dtype=torch.float64, device="cuda")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _topk_match(d_o.cpu().numpy().reshape(w, 8, 4), oracle.batch_topk(s, n, n, "none", "hann", 0, None, 8, 18, 200),
+                1e-10)
+    plan.close()
