@@ -140,7 +140,7 @@ void pool_release_all() {
 }
 
 // ----------------------------------------------------------------- tables
-// W_N^k = exp(-2 pi i k/N), k < N/2, rounded once from long double.
+// W_N^k = exp(-2 pi i k/N), k < N, rounded once from long double.
 // Window coefficients: the exact expressions of L/WaveSpecZZ_1.0.2.mq5:884-922
 // evaluated in double on the host (bit-identical to the CPU path).
 double window_value(int type, int i, int n) {
@@ -170,8 +170,8 @@ int get_tables(int dev, int log2n, int window, bool f32, Tables *out) {
     }
     const int n = 1 << log2n;
     const size_t es = f32 ? sizeof(float) : sizeof(double);
-    std::vector<char> tw((size_t)n / 2 * 2 * es), win((size_t)n * es);
-    for (int k = 0; k < n / 2; ++k) {
+    std::vector<char> tw((size_t)n * 2 * es), win((size_t)n * es);
+    for (int k = 0; k < n; ++k) {  // full period: table-loaded twiddle powers index up to N-1
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)k / (long double)n;
         const long double c = cosl(ang), s = sinl(ang);
         if (f32) {

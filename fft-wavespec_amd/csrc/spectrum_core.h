@@ -147,18 +147,19 @@ template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int bas
 
 // Window classes: none; a0 + a1 cos th + a2 cos 2th (Hann, Hamming, Blackman);
 // Bartlett (evaluated exactly as L/WaveSpecZZ_1.0.2.mq5:918-922).
-enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2 };
+enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2, kWinCos2 = 3 };  // kWinCos: a2 = 0
 // Ablation bits (tools/kbench.hip only; the library uses 0).
 enum Var : int {
     kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32,
     kVarSplitLds = 64,  // real/imaginary halves exchanged separately: half the LDS, 3 waves/SIMD
     kVarOcc4 = 128,     // with kVarSplitLds: 4 waves/SIMD (8 workgroups/CU, <= 128 VGPRs)
+    kVarTwTable = 256,  // twiddle powers loaded from the W_N^k table instead of product chains
 };
 
 template <typename T> struct SpecArgs {
     const T *__restrict__ series;
     T *__restrict__ out;
-    const cpx<T> *__restrict__ tw;  // W_N^k, k < N/2
+    const cpx<T> *__restrict__ tw;  // W_N^k, k < N
     int64_t hop, n_windows, n_groups;
     int vec;                         // 16-B (8-B for f32) pair loads are aligned
     int nt;                          // windows do not overlap: stream with non-temporal loads
@@ -232,7 +233,25 @@ __device__ __forceinline__ void exchange(char *base, cpx<T> (&v)[16], int t) {
 
 // Stockham pass 0 < PASS < NPASS-1 on data already in its read layout:
 // twiddle W^(r (b mod Ns)) then in-register radix-R DFTs, then the exchange.
-template <bool SPLIT, typename T, int LOG2N, int PASS>
+// Multiplies v[r] (r = 1..R-1) by W_N^(r*k1): product chain of the base
+// twiddle (VALU) or one table load per power (TABLE; |r*k1| < N).
+template <bool TABLE, typename T, int R>
+__device__ __forceinline__ void twiddle(cpx<T> *v, const cpx<T> *__restrict__ tw, int k1) {
+    if constexpr (TABLE) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k1]);
+    } else {
+        const cpx<T> w = tw[k1];
+        cpx<T> wr = w;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+            v[r] = cmul(v[r], wr);
+            if (r + 1 < R) wr = cmul(wr, w);
+        }
+    }
+}
+
+template <bool SPLIT, bool TABLE, typename T, int LOG2N, int PASS>
 __device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cpx<T> *__restrict__ tw, int t) {
     using G = Geo<LOG2N>;
     if constexpr (PASS < G::NPASS - 1) {
@@ -240,17 +259,11 @@ __device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cp
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
             const int b = t + G::TPW * q;
-            const cpx<T> w = tw[(b % Ns) * (G::N / (Ns * R))];
-            cpx<T> wr = w;
-#pragma unroll
-            for (int r = 1; r < R; ++r) {
-                v[q * R + r] = cmul(v[q * R + r], wr);
-                if (r + 1 < R) wr = cmul(wr, w);
-            }
+            twiddle<TABLE, T, R>(&v[q * R], tw, (b % Ns) * (G::N / (Ns * R)));
             dft<T, R>(&v[q * R]);
         }
         exchange<SPLIT, T, LOG2N, PASS>(base, v, t);
-        mid_passes<SPLIT, T, LOG2N, PASS + 1>(base, v, tw, t);
+        mid_passes<SPLIT, TABLE, T, LOG2N, PASS + 1>(base, v, tw, t);
     }
 }
 
@@ -306,8 +319,9 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
     char *lbase = smem + slot * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));  // this window's LDS slot
 
     // per-thread window rotation start: th_i at i = 2 (t + TPW q)
+    constexpr bool kCosWin = WCLASS == kWinCos || WCLASS == kWinCos2;
     double wc0[BPT0], ws0[BPT0];
-    if constexpr (WCLASS == kWinCos) {
+    if constexpr (kCosWin) {
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) sincos(a.inv_theta * (double)(2 * (t + TPW * q)), &ws0[q], &wc0[q]);
     }
@@ -426,7 +440,7 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) {
             double c = 0.0, s = 0.0;
-            if constexpr (WCLASS == kWinCos) {
+            if constexpr (kCosWin) {
                 c = wc0[q];
                 s = ws0[q];
                 asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no 64-VGPR hoist
@@ -434,10 +448,15 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 double da = xa[q * R0 + r], db = xb[q * R0 + r];
-                if constexpr (WCLASS == kWinCos) {
+                if constexpr (kCosWin) {
                     const double co = c * a.co - s * a.so;  // th_(i+1)
-                    da *= a.a0 + a.a1 * c + a.a2 * (2.0 * c * c - 1.0);
-                    db *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                    if constexpr (WCLASS == kWinCos2) {      // Blackman: + a2 cos 2th
+                        da *= a.a0 + a.a1 * c + a.a2 * (2.0 * c * c - 1.0);
+                        db *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                    } else {                                 // Hann 0.5(1 - cos), Hamming
+                        da *= a.a0 + a.a1 * c;
+                        db *= a.a0 + a.a1 * co;
+                    }
                     const double cn = c * a.cs - s * a.ss;
                     s = s * a.cs + c * a.ss;
                     c = cn;
@@ -482,7 +501,7 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) dft<T, R0>(&v[q * R0]);
         exchange<kSplit, T, LOG2N, 0>(lbase, v, t);  // also orders the previous group's reads
-        mid_passes<kSplit, T, LOG2N, 1>(lbase, v, a.tw, t);
+        mid_passes<kSplit, (VAR & kVarTwTable) != 0, T, LOG2N, 1>(lbase, v, a.tw, t);
 
         // ---- final radix-8 pass: thread t owns butterflies {t, B-t} ({0, B/2} for t = 0)
         const int bq0 = t, bq1 = t == 0 ? TPW : 2 * TPW - t;
@@ -492,18 +511,9 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
             u0[r] = v[r];
             u1[r] = v[8 + r];
         }
-        if constexpr (G::NPASS > 1) {
-            const cpx<T> w0 = a.tw[2 * bq0], w1 = a.tw[2 * bq1];  // (b % Ns) * N/(Ns*8) with Ns = B
-            cpx<T> wr0 = w0, wr1 = w1;
-#pragma unroll
-            for (int r = 1; r < 8; ++r) {
-                u0[r] = cmul(u0[r], wr0);
-                u1[r] = cmul(u1[r], wr1);
-                if (r + 1 < 8) {
-                    wr0 = cmul(wr0, w0);
-                    wr1 = cmul(wr1, w1);
-                }
-            }
+        if constexpr (G::NPASS > 1) {  // (b % Ns) * N/(Ns*8) = 2b with Ns = B
+            twiddle<(VAR & kVarTwTable) != 0, T, 8>(u0, a.tw, 2 * bq0);
+            twiddle<(VAR & kVarTwTable) != 0, T, 8>(u1, a.tw, 2 * bq1);
         }
         dft<T, 8>(u0);
         dft<T, 8>(u1);

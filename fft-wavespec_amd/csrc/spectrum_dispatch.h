@@ -14,7 +14,7 @@ inline int window_class(int window, double *a0, double *a1, double *a2) {
     switch (window) {
     case 1: *a0 = 0.5, *a1 = -0.5; return kWinCos;                  // Hann 0.5(1 - cos)
     case 2: *a0 = 0.54, *a1 = -0.46; return kWinCos;                // Hamming
-    case 3: *a0 = 0.42, *a1 = -0.5, *a2 = 0.08; return kWinCos;     // Blackman
+    case 3: *a0 = 0.42, *a1 = -0.5, *a2 = 0.08; return kWinCos2;    // Blackman
     case 4: return kWinBartlett;
     default: return kWinNone;
     }
@@ -90,6 +90,7 @@ hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
     double a0, a1, a2;
     switch (window_class(L.window, &a0, &a1, &a2)) {
     case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos>(L, s);
+    case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2>(L, s);
     case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett>(L, s);
     default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone>(L, s);
     }

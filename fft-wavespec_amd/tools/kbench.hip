@@ -145,8 +145,57 @@ int kalman_main(int reps) {
     return 0;
 }
 
+template <int VAR>
+float time_c4(const SpectrumLaunch &L, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK((launch_one<double, 11, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) CK((launch_one<double, 11, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1000.f / reps;
+}
+
+// C4 shape: 1M windows x 2048, hop = 1 (compute-bound)
+int c4_main(int reps) {
+    const int64_t W = 1 << 20;
+    const int n = 2048;
+    double *x, *out, *tw;
+    CK(hipMalloc(&x, (W + n) * 8));
+    CK(hipMalloc(&out, W * n / 2 * 8));
+    CK(hipMalloc(&tw, n * 16));
+    std::vector<double> h(2 * n);
+    for (int k = 0; k < n; ++k) {
+        long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+        h[2 * k] = (double)cosl(a);
+        h[2 * k + 1] = (double)sinl(a);
+    }
+    CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_walk, dim3(1024), dim3(256), 0, 0, x, W + n);
+    CK(hipDeviceSynchronize());
+    SpectrumLaunch L{};
+    L.series = x; L.out = out; L.twiddle = tw; L.window = 1; L.hop = 1; L.n_windows = W; L.log2n = 11;
+    const double bytes = (W + n) * 8.0 + W * (n / 2) * 8.0;
+    for (int round = 0; round < 2; ++round)
+        for (int g : {16384, 32768, 65536}) {
+            L.grid = g;
+            const float a = time_c4<kVarSplitLds | kVarNoPrefetch | kVarNtStore>(L, reps);
+            const float b = time_c4<kVarSplitLds | kVarNoPrefetch | kVarNtStore | kVarTwTable>(L, reps);
+            const float c = time_c4<kVarNoPrefetch | kVarNtStore>(L, reps);
+            printf("round %d c4 grid=%6d  split %8.1f us (%6.1f GB/s)  split+twtab %8.1f us  aos %8.1f us\n", round, g, a,
+                   bytes / a / 1e3, b, c);
+            fflush(stdout);
+        }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "kalman") return kalman_main(argc > 2 ? atoi(argv[2]) : 5);
+    if (argc > 1 && std::string(argv[1]) == "c4") return c4_main(argc > 2 ? atoi(argv[2]) : 5);
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;
@@ -155,14 +204,14 @@ int main(int argc, char **argv) {
     double *x, *out, *tw;
     CK(hipMalloc(&x, len * 8));
     CK(hipMalloc(&out, W * n / 2 * 8));
-    CK(hipMalloc(&tw, n / 2 * 16));
-    std::vector<double> h(n);
-    for (int k = 0; k < n / 2; ++k) {
+    CK(hipMalloc(&tw, n * 16));
+    std::vector<double> h(2 * n);
+    for (int k = 0; k < n; ++k) {
         long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
         h[2 * k] = (double)cosl(a);
         h[2 * k + 1] = (double)sinl(a);
     }
-    CK(hipMemcpy(tw, h.data(), n * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(fill_walk, dim3(4096), dim3(256), 0, 0, x, len);
     CK(hipDeviceSynchronize());
     hipStream_t s;
@@ -221,9 +270,8 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[4] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"split+occ4+nt2", time_variant<kVarSplitLds | kVarOcc4 | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
-                      {"split+blk+nt2", time_variant<kVarSplitLds | kVarBlocked | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+            } r[3] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+nt2+twtab", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore | kVarTwTable>(L, s, reps)},
                       {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)}};
             for (auto &v : r)
                 printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s  %.3f of 8TB/s\n", round, v.name, g, v.us,

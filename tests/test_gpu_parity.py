@@ -236,13 +236,14 @@ def test_golden_vectors_on_gpu(gpu_session, path):
     assert oracle.rel_err(p, g["power"]) <= 1e-10
 
 
-def _topk_match(got, want, tol):
+def _topk_match(got, want, tol, full_max):
     """Bins identical except where two candidates' powers tie within tol (the order of a near-tie
-    is decided by rounding); powers and Re/Im within tol of the oracle's."""
+    is decided by rounding); powers and Re/Im within tol -- normalised, like every parity check
+    here, by the window's full-spectrum max power."""
     assert got.shape == want.shape
     for w in range(got.shape[0]):
         gb, wb = got[w, :, 0].astype(int), want[w, :, 0].astype(int)
-        scale = max(want[w, 0, 1], 1e-300)
+        scale = max(full_max[w], 1e-300)
         for s in np.nonzero(gb != wb)[0]:
             assert abs(got[w, s, 1] - want[w, s, 1]) <= tol * scale, (w, s, gb, wb)
         assert np.max(np.abs(got[w, :, 1] - want[w, :, 1])) <= tol * scale
@@ -259,7 +260,7 @@ def test_topk_scan(gpu_session, n, hop, k, minp, maxp, detrend):
     s = synth.random_walk((40 - 1) * hop + n, seed=n + k)
     got = bridge.spectrum_topk_batch(s, n, hop, detrend, "hann", 1024, "f64", k, minp, maxp)
     want = oracle.batch_topk(s, n, hop, detrend, "hann", 1024, None, k, minp, maxp)
-    _topk_match(got, want, 1e-10)
+    _topk_match(got, want, 1e-10, ref(s, n, hop, detrend, "hann", 1024).max(axis=1))
 
 
 def test_topk_f32_and_plan(gpu_session):
@@ -267,8 +268,9 @@ def test_topk_f32_and_plan(gpu_session):
     n, w = 2048, 300
     s = synth.random_walk(n * w, seed=3)
     got = bridge.spectrum_topk_batch(s, n, n, "none", "hann", 0, "f32", 8, 18, 200)
-    want = oracle.batch_topk(s.astype(np.float32).astype(np.float64), n, n, "none", "hann", 0, None, 8, 18, 200)
-    _topk_match(got, want, 1e-5)
+    s32 = s.astype(np.float32).astype(np.float64)
+    want = oracle.batch_topk(s32, n, n, "none", "hann", 0, None, 8, 18, 200)
+    _topk_match(got, want, 1e-5, ref(s32, n, n).max(axis=1))
     plan = bridge.Plan(0, n, n, w, "none", "hann")
     plan.set_topk(8, 18, 200)
     d_s = torch.from_numpy(s).cuda()
@@ -276,5 +278,5 @@ def test_topk_f32_and_plan(gpu_session):
     plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     _topk_match(d_o.cpu().numpy().reshape(w, 8, 4), oracle.batch_topk(s, n, n, "none", "hann", 0, None, 8, 18, 200),
-                1e-10)
+                1e-10, ref(s, n, n).max(axis=1))
     plan.close()
