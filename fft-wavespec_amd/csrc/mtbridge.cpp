@@ -130,39 +130,27 @@ void host_free(void *p, size_t bytes) {
 void pool_release_all() {
     std::lock_guard<std::mutex> lk(pool().mu);
     for (auto &kv : pool().free_dev) {
-        hipSetDevice(kv.first.first);
-        for (void *p : kv.second) hipFree(p);
+        (void)hipSetDevice(kv.first.first);
+        for (void *p : kv.second) (void)hipFree(p);
     }
     pool().free_dev.clear();
     for (auto &kv : pool().free_host)
-        for (void *p : kv.second) hipHostFree(p);
+        for (void *p : kv.second) (void)hipHostFree(p);
     pool().free_host.clear();
 }
 
 // ----------------------------------------------------------------- tables
-// W_N^k = exp(-2 pi i k/N), k < N, rounded once from long double.
-// Window coefficients: the exact expressions of L/WaveSpecZZ_1.0.2.mq5:884-922
-// evaluated in double on the host (bit-identical to the CPU path).
-double window_value(int type, int i, int n) {
-    switch (type) {
-    case MTB_WINDOW_HANN: return 0.5 * (1.0 - cos(2.0 * M_PI * i / (n - 1)));
-    case MTB_WINDOW_HAMMING: return 0.54 - 0.46 * cos(2.0 * M_PI * i / (n - 1));
-    case MTB_WINDOW_BLACKMAN: return 0.42 - 0.5 * cos(2.0 * M_PI * i / (n - 1)) + 0.08 * cos(4.0 * M_PI * i / (n - 1));
-    case MTB_WINDOW_BARTLETT: return 1.0 - fabs((2.0 * i - n + 1) / (n - 1));
-    default: return 1.0;
-    }
-}
-
+// W_N^k = exp(-2 pi i k/N), k < N, rounded once from long double.  (Window
+// coefficients are generated in the kernel by a rotation recurrence.)
 struct Tables {
     void *tw = nullptr;
-    void *win = nullptr;  // null = rectangular
 };
 std::mutex g_tables_mu;
-std::map<std::tuple<int, int, int, bool>, Tables> *g_tables = new std::map<std::tuple<int, int, int, bool>, Tables>();
+std::map<std::tuple<int, int, bool>, Tables> *g_tables = new std::map<std::tuple<int, int, bool>, Tables>();
 
-int get_tables(int dev, int log2n, int window, bool f32, Tables *out) {
+int get_tables(int dev, int log2n, bool f32, Tables *out) {
     std::lock_guard<std::mutex> lk(g_tables_mu);
-    auto key = std::make_tuple(dev, log2n, window, f32);
+    auto key = std::make_tuple(dev, log2n, f32);
     auto it = g_tables->find(key);
     if (it != g_tables->end()) {
         *out = it->second;
@@ -170,7 +158,7 @@ int get_tables(int dev, int log2n, int window, bool f32, Tables *out) {
     }
     const int n = 1 << log2n;
     const size_t es = f32 ? sizeof(float) : sizeof(double);
-    std::vector<char> tw((size_t)n * 2 * es), win((size_t)n * es);
+    std::vector<char> tw((size_t)n * 2 * es);
     for (int k = 0; k < n; ++k) {  // full period: table-loaded twiddle powers index up to N-1
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)k / (long double)n;
         const long double c = cosl(ang), s = sinl(ang);
@@ -182,33 +170,34 @@ int get_tables(int dev, int log2n, int window, bool f32, Tables *out) {
             ((double *)tw.data())[2 * k + 1] = (double)s;
         }
     }
-    for (int i = 0; i < n; ++i) {
-        const double wv = window_value(window, i, n);
-        if (f32) ((float *)win.data())[i] = (float)wv;
-        else ((double *)win.data())[i] = wv;
-    }
     Tables t;
     HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
     HIP_OR(hipMalloc(&t.tw, tw.size()), MTB_NO_MEM);
     HIP_OR(hipMemcpy(t.tw, tw.data(), tw.size(), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
-    if (window != MTB_WINDOW_NONE) {
-        HIP_OR(hipMalloc(&t.win, win.size()), MTB_NO_MEM);
-        HIP_OR(hipMemcpy(t.win, win.data(), win.size(), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
-    }
     (*g_tables)[key] = t;
     *out = t;
     return MTB_OK;
 }
 
 // ----------------------------------------------------------------- config
+enum Op : int { kOpSpectrum = 0, kOpInverse = 1 };
 struct Config {
+    int op = kOpSpectrum;  // kOpInverse: rows of packed spectra -> rows of samples
     int n = 0, log2n = 0;
     int64_t hop = 0, n_windows = 0;
     int detrend = 0, window = 0, trend_period = 0, output = 0;
-    int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK
+    int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK / MTB_OUT_TOPK_PHASE
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
-    int64_t record() const { return output == MTB_OUT_PACKED ? n : output == MTB_OUT_TOPK ? 4 * topk : n / 2; }
+    int64_t record() const {
+        if (op == kOpInverse || output == MTB_OUT_PACKED) return n;
+        switch (output) {
+        case MTB_OUT_TOPK: return 4 * topk;
+        case MTB_OUT_TOPK_PHASE: return 6 * topk;
+        case MTB_OUT_PHASE: return 3 * (n / 2);
+        default: return n / 2;
+        }
+    }
     int64_t series_elems() const { return (n_windows - 1) * hop + n; }
     int64_t unique_input_elems() const { return hop >= n ? n_windows * (int64_t)n : series_elems(); }
 };
@@ -235,8 +224,12 @@ int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int
     }
     if (detrend < MTB_DETREND_NONE || detrend > MTB_DETREND_KALMAN || window < MTB_WINDOW_NONE ||
         window > MTB_WINDOW_BARTLETT || (precision != MTB_PREC_F64 && precision != MTB_PREC_F32) ||
-        (output != MTB_OUT_POWER && output != MTB_OUT_PACKED && output != MTB_OUT_TOPK)) {
+        output < MTB_OUT_POWER || output > MTB_OUT_TOPK_PHASE) {
         set_error("bad mode: detrend=%d window=%d precision=%d output=%d", detrend, window, precision, output);
+        return MTB_BAD_ARGS;
+    }
+    if ((output == MTB_OUT_PHASE || output == MTB_OUT_TOPK_PHASE) && precision != MTB_PREC_F64) {
+        set_error("output=%d (phase) is computed in fp64 only", output);
         return MTB_BAD_ARGS;
     }
     c->n = window_len;
@@ -251,7 +244,7 @@ int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int
     c->f32 = precision == MTB_PREC_F32;
     // MTB_OUT_TOPK through the generic entry points: the reference's own scan
     // parameters (top 8, InpMinPeriod 18 / InpMaxPeriod 200, 1.1.0:22-23)
-    if (output == MTB_OUT_TOPK) return config_set_topk(c, 8, 18.0, 200.0);
+    if (output == MTB_OUT_TOPK || output == MTB_OUT_TOPK_PHASE) return config_set_topk(c, 8, 18.0, 200.0);
     return MTB_OK;
 }
 
@@ -262,7 +255,7 @@ int config_set_topk(Config *c, int top_k, double min_period, double max_period) 
                   min_period, max_period);
         return MTB_BAD_ARGS;
     }
-    c->output = MTB_OUT_TOPK;
+    if (c->output != MTB_OUT_TOPK_PHASE) c->output = MTB_OUT_TOPK;
     c->topk = top_k;
     c->kmin = (int)ceil((double)c->n / max_period);
     c->kmax = (int)floor((double)c->n / min_period);
@@ -280,9 +273,19 @@ double g_kalman[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.
 int enqueue(int dev, const Config &c, const double *kalman, const void *d_series, void *d_out, void *d_ws,
             hipStream_t s) {
     Tables t;
-    int st = get_tables(dev, c.log2n, c.window, c.f32, &t);
+    int st = get_tables(dev, c.log2n, c.f32, &t);
     if (st != MTB_OK) return st;
     HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    if (c.op == kOpInverse) {
+        InverseLaunch I{};
+        I.in = static_cast<const double *>(d_series);
+        I.out = static_cast<double *>(d_out);
+        I.twiddle = t.tw;
+        I.n_windows = c.n_windows;
+        I.log2n = c.log2n;
+        HIP_OR(launch_inverse(I, s), MTB_INTERNAL_ERROR);
+        return MTB_OK;
+    }
     SpectrumLaunch L{};
     L.series = d_series;
     L.hop = c.hop;
@@ -373,9 +376,9 @@ struct Batch {
     ~Batch() {
         for (auto &p : parts) {
             if (p.done) {
-                hipSetDevice(p.dev);
-                hipEventSynchronize(p.done);
-                hipEventDestroy(p.done);
+                (void)hipSetDevice(p.dev);
+                (void)hipEventSynchronize(p.done);
+                (void)hipEventDestroy(p.done);
             }
             dev_free(p.dev, p.d_in, p.in_bytes);
             dev_free(p.dev, p.d_out, p.out_bytes);
@@ -446,7 +449,7 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
 // unless `wait`).
 int batch_poll(Batch &b, bool wait) {
     for (auto &p : b.parts) {
-        hipSetDevice(p.dev);
+        (void)hipSetDevice(p.dev);
         hipError_t e = wait ? hipEventSynchronize(p.done) : hipEventQuery(p.done);
         if (e == hipErrorNotReady) return MTB_NOT_READY;
         if (e != hipSuccess) {
@@ -555,10 +558,10 @@ MTB_API void gpu_shutdown(void) {
     }
     if (S) {
         for (auto &D : S->devs) {
-            hipSetDevice(D->dev);
+            (void)hipSetDevice(D->dev);
             for (auto st : D->streams) {
-                hipStreamSynchronize(st);
-                hipStreamDestroy(st);
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
             }
         }
     }
@@ -588,6 +591,75 @@ MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len,
     if (st != MTB_OK) return st;
     int32_t n = 0;
     return run_sync(c, in, out, (int64_t)window_len * n_windows, &n);
+}
+
+static int inverse_config(int32_t window_len, int32_t n_windows, Config *c) {
+    int st = make_config(window_len, window_len, n_windows, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64,
+                         MTB_OUT_PACKED, c);
+    c->op = kOpInverse;
+    return st;
+}
+
+MTB_API int32_t gpu_fft_real_inverse(const double *in_spec, int32_t len, double *out) {
+    if (!in_spec || !out) {
+        set_error("gpu_fft_real_inverse: null buffer");
+        return MTB_BAD_ARGS;
+    }
+    Config c;
+    int st = inverse_config(len, 1, &c);
+    if (st != MTB_OK) return st;
+    int32_t n = 0;
+    return run_sync(c, in_spec, out, len, &n);
+}
+
+MTB_API int32_t gpu_fft_real_inverse_batch(const double *in, int32_t window_len, int32_t n_windows, double *out) {
+    if (!in || !out) {
+        set_error("gpu_fft_real_inverse_batch: null buffer");
+        return MTB_BAD_ARGS;
+    }
+    Config c;
+    int st = inverse_config(window_len, n_windows, &c);
+    if (st != MTB_OK) return st;
+    int32_t n = 0;
+    return run_sync(c, in, out, (int64_t)window_len * n_windows, &n);
+}
+
+MTB_API int32_t gpu_spectral_phase_unwrap(const double *spectrum, int32_t spectrum_len, int32_t method, double *out,
+                                          int32_t out_len) {
+    if (!spectrum || !out || spectrum_len < 2 || (spectrum_len & 1) || method < 0 || method > 2 ||
+        out_len < spectrum_len / 2) {
+        set_error("gpu_spectral_phase_unwrap: spectrum_len=%d (even, >= 2) method=%d (0..2) out_len=%d (>= %d)",
+                  spectrum_len, method, out_len, spectrum_len / 2);
+        return MTB_BAD_ARGS;
+    }
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    DeviceCtx &D = *S->devs[0];
+    const int nb = spectrum_len / 2;
+    const size_t in_bytes = (size_t)spectrum_len * sizeof(double), out_bytes = (size_t)nb * sizeof(double);
+    HIP_OR(hipSetDevice(D.dev), MTB_BACKEND_UNAVAILABLE);
+    void *d_in = dev_alloc(D.dev, in_bytes), *d_out = dev_alloc(D.dev, out_bytes);
+    if (!d_in || !d_out) {
+        dev_free(D.dev, d_in, in_bytes);
+        dev_free(D.dev, d_out, out_bytes);
+        return MTB_NO_MEM;
+    }
+    const hipStream_t s = D.next_stream();
+    int st = MTB_OK;
+    hipError_t e = hipMemcpyAsync(d_in, spectrum, in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_phase_row((const double *)d_in, nb, method, (double *)d_out, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        set_error("gpu_spectral_phase_unwrap: %s", hipGetErrorString(e));
+        st = MTB_INTERNAL_ERROR;
+    }
+    dev_free(D.dev, d_in, in_bytes);
+    dev_free(D.dev, d_out, out_bytes);
+    return st;
 }
 
 static int spectrum_config(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
@@ -630,6 +702,25 @@ MTB_API int32_t gpu_spectrum_topk_batch(const double *series, int32_t series_len
     Config c;
     int st = spectrum_config(series, series_len, window_len, hop, detrend, window, trend_period, precision,
                              MTB_OUT_POWER, &c);
+    if (st != MTB_OK) return st;
+    st = config_set_topk(&c, top_k, min_period, max_period);
+    if (st != MTB_OK) return st;
+    if (!out || out_cap < c.record()) {
+        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)c.record());
+        return MTB_BAD_ARGS;
+    }
+    c.n_windows = std::min<int64_t>(c.n_windows, out_cap / c.record());
+    return run_sync(c, series, out, out_cap, out_len);
+}
+
+MTB_API int32_t gpu_spectrum_topk_phase_batch(const double *series, int32_t series_len, int32_t window_len,
+                                              int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
+                                              int32_t top_k, double min_period, double max_period, double *out,
+                                              int32_t out_cap, int32_t *out_len) {
+    if (out_len) *out_len = 0;
+    Config c;
+    int st = spectrum_config(series, series_len, window_len, hop, detrend, window, trend_period, MTB_PREC_F64,
+                             MTB_OUT_TOPK_PHASE, &c);
     if (st != MTB_OK) return st;
     st = config_set_topk(&c, top_k, min_period, max_period);
     if (st != MTB_OK) return st;
@@ -779,7 +870,7 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
         memcpy(p->kalman, g_kalman, sizeof(g_kalman));
     }
     Tables t;
-    if (get_tables(device, p->cfg.log2n, p->cfg.window, p->cfg.f32, &t) != MTB_OK) return 0;
+    if (get_tables(device, p->cfg.log2n, p->cfg.f32, &t) != MTB_OK) return 0;
     if (p->cfg.detrend == MTB_DETREND_KALMAN) {
         p->ws_bytes = (size_t)(p->cfg.n_windows * p->cfg.n) * p->cfg.elem();
         if (hipSetDevice(device) != hipSuccess || hipMalloc(&p->d_ws, p->ws_bytes) != hipSuccess) {
@@ -787,6 +878,30 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
             return 0;
         }
     }
+    const int64_t id = g_next_id.fetch_add(1);
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    (*g_plans)[id] = std::move(p);
+    return id;
+}
+
+MTB_API int64_t wsp_plan_create_inverse(int32_t device, int32_t window_len, int64_t n_windows) {
+    const int n = device_count();
+    if (n <= 0) {
+        set_error("no HIP device visible; the inverse path has no CPU fallback");
+        return 0;
+    }
+    if (device < 0 || device >= n) {
+        set_error("device %d out of range (%d devices)", device, n);
+        return 0;
+    }
+    auto p = std::make_unique<Plan>();
+    if (make_config(window_len, window_len, n_windows, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64,
+                    MTB_OUT_PACKED, &p->cfg) != MTB_OK)
+        return 0;
+    p->cfg.op = kOpInverse;
+    p->dev = device;
+    Tables t;
+    if (get_tables(device, p->cfg.log2n, false, &t) != MTB_OK) return 0;
     const int64_t id = g_next_id.fetch_add(1);
     std::lock_guard<std::mutex> lk(g_plans_mu);
     (*g_plans)[id] = std::move(p);
@@ -818,6 +933,10 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
         set_error("unknown plan %lld", (long long)plan);
         return MTB_BAD_ARGS;
     }
+    if (it->second->cfg.op != kOpSpectrum) {
+        set_error("plan %lld is not a spectrum plan", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
     return config_set_topk(&it->second->cfg, top_k, min_period, max_period);
 }
 
@@ -842,9 +961,9 @@ MTB_API int32_t wsp_plan_destroy(int64_t plan) {
         g_plans->erase(it);
     }
     if (p->d_ws) {
-        hipSetDevice(p->dev);
-        hipDeviceSynchronize();
-        hipFree(p->d_ws);
+        (void)hipSetDevice(p->dev);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(p->d_ws);
     }
     return MTB_OK;
 }

@@ -167,7 +167,7 @@ template <typename T> struct SpecArgs {
     // by (co, so) from an even to the next odd sample
     double a0, a1, a2, cs, ss, co, so, inv_theta;  // inv_theta = 2 pi/(N-1)
     double inv_nm1;                  // 1/(N-1) for Bartlett
-    int topk, kmin, kmax;            // kOutTopK: k slots over bins [kmin, kmax]
+    int topk, kmin, kmax;            // kOutTopK(Phase): k slots over bins [kmin, kmax]
     double alpha, c;                 // IIR trend (L/WaveSpecZZ_1.0.2.mq5:3041-3043)
     double apow[8];                  // alpha^(32 * 2^j)
 };
@@ -267,6 +267,75 @@ __device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cp
     }
 }
 
+// Phase, unwrap and group delay of one window (CalculateFFTPhase, UnwrapPhase,
+// CalculateGroupDelay: L/WaveSpecZZ_1.0.4-new.mq5:1040-1120, called at :3225-3227
+// with n = N over the GPU unpack of :3183-3196, i.e. X_k for k < N/2 and zeros
+// above).  X is staged in LDS at xrow[pad16(k)]; thread t owns bins
+// [16t, 16t + 16) (TPW = M/16) and recomputes the phase of its two neighbour
+// bins itself.  The reference's sequential unwrap u_i = u_(i-1) + diff + corr
+// equals phi_i + 2 pi K_i with K_i the running count of +-1 corrections: K is
+// an exact integer prefix scan and u is one fma, so only the rounding of the
+// reference's running sum (not its decisions) differs.
+template <int LOG2N>
+__device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, double *scanbuf, double (&pw)[16],
+                                            double (&u)[16], double (&gd)[16]) {
+    using G = Geo<LOG2N>;
+    constexpr int M = G::M, TPW = G::TPW;
+    constexpr double kPi = 3.14159265358979323846;  // M_PI
+    constexpr double k2Pi = 2.0 * kPi;              // the reference's 2.0 * M_PI correction
+    const int k0 = 16 * t;
+    double ph[18];  // bins k0 - 1 .. k0 + 16
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+        const int k = k0 - 1 + j;
+        ph[j] = 0.0;  // bin M: the zeroed upper half, atan2(0, 0) = 0
+        if (k >= 0 && k < M) {
+            const cpx<double> x = xrow[pad16(k)];
+            ph[j] = atan2(x.im, x.re);
+            if (j >= 1 && j <= 16) pw[j - 1] = x.re * x.re + x.im * x.im;
+        }
+    }
+    int cj[17];  // correction count of bins k0 .. k0 + 16 (UnwrapPhase :1068-1077)
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const double diff = ph[j + 1] - ph[j];
+        cj[j] = (k0 + j == 0) ? 0 : diff > kPi ? -1 : diff < -kPi ? 1 : 0;
+    }
+    int sum = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sum += cj[j];
+    constexpr int SW = TPW < 64 ? TPW : 64;
+    const int lt = t & (SW - 1);
+    int incl = sum;
+#pragma unroll
+    for (int d = 1; d < SW; d <<= 1) {
+        const int up = __shfl_up(incl, d, SW);
+        if (lt >= d) incl += up;
+    }
+    int K = incl - sum;  // corrections of every bin < k0
+    if constexpr (TPW == 128) {
+        int *sb = reinterpret_cast<int *>(scanbuf + 4);
+        if (t == 63) sb[0] = incl;
+        __syncthreads();
+        if (t >= 64) K += sb[0];
+    }
+    const double um1 = fma((double)K, k2Pi, ph[0]);  // u[k0 - 1]
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        K += cj[j];
+        u[j] = fma((double)K, k2Pi, ph[j + 1]);
+    }
+    const double up16 = fma((double)(K + cj[16]), k2Pi, ph[17]);  // u[k0 + 16]
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // :1102-1119 (n = N >= 32: every bin < M has two neighbours but bin 0)
+        const double lo = j ? u[j - 1] : um1, hi = j < 15 ? u[j + 1] : up16;
+        double g = (k0 + j == 0) ? -(u[1] - u[0]) : -(hi - lo) / 2.0;
+        if (g > 100.0) g = 100.0;
+        if (g < -100.0) g = -100.0;
+        gd[j] = g;
+    }
+}
+
 // Loads the 16 sample pairs of this thread for group g (pass-0 layout,
 // element (q, r) = z[(t + TPW q) + (M/R0) r]).  Inactive slots read window 0.
 template <typename T, int LOG2N, int VAR = 0>
@@ -310,6 +379,8 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
     constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
     constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
     constexpr int kScan = 16 * 8;
+    constexpr bool kPhase = OUT == kOutPhase || OUT == kOutTopKPhase;
+    static_assert(!kPhase || sizeof(T) == 8, "phase outputs are fp64");
     __shared__ __attribute__((aligned(16))) char smem[kMain + kScan];
     double *scanbuf = reinterpret_cast<double *>(smem + kMain);
 
@@ -568,10 +639,10 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
             if constexpr (OUT == kOutPower) {
                 prow[ka] = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
                 prow[kb] = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
-            } else if constexpr (OUT == kOutTopK) {  // stage X for the scan (AoS slot)
+            } else if constexpr (OUT == kOutTopK || kPhase) {  // stage X for the scan (AoS slot)
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
-                xrow[ka] = {T(0.5) * xa.re, T(0.5) * xa.im};
-                xrow[kb] = {T(0.5) * xb.re, T(0.5) * xb.im};
+                xrow[kPhase ? pad16(ka) : ka] = {T(0.5) * xa.re, T(0.5) * xa.im};
+                xrow[kPhase ? pad16(kb) : kb] = {T(0.5) * xb.re, T(0.5) * xb.im};
             } else if (active) {  // packed: (Re, Im) of one bin is already one 16-B (8-B) store
                 v2 oa, ob;
                 oa.x = T(0.5) * xa.re;
@@ -582,7 +653,27 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
                 *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
             }
         }
-        if constexpr (OUT == kOutTopK) {
+        // unwrapped phase / group delay of bins [16t, 16t + 16) (kept in registers
+        // through the top-k scan for kOutTopKPhase)
+        double pw[kPhase ? 16 : 1], u[kPhase ? 16 : 1], gd[kPhase ? 16 : 1];
+        if constexpr (kPhase) {
+            const cpx<double> *xrow = reinterpret_cast<const cpx<double> *>(lbase);
+            __syncthreads();  // X row complete
+            phase_chunk<LOG2N>(xrow, t, scanbuf, pw, u, gd);
+            if constexpr (OUT == kOutPhase) {
+                // record [P | unwrapped phase | group delay]: 16 contiguous bins per lane
+                if (active) {
+                    T *rec = a.out + w * (int64_t)(3 * M) + 16 * t;
+#pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        __builtin_nontemporal_store(v2{pw[j], pw[j + 1]}, reinterpret_cast<v2 *>(rec + j));
+                        __builtin_nontemporal_store(v2{u[j], u[j + 1]}, reinterpret_cast<v2 *>(rec + M + j));
+                        __builtin_nontemporal_store(v2{gd[j], gd[j + 1]}, reinterpret_cast<v2 *>(rec + 2 * M + j));
+                    }
+                }
+            }
+        }
+        if constexpr (OUT == kOutTopK || OUT == kOutTopKPhase) {
             // Top-k bin scan (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554):
             // k rounds of argmax over bins [kmin, kmax] ordered (power desc, bin asc) -- the
             // order the reference's strict-'>' insertion in ascending bin order produces.  The
@@ -590,12 +681,14 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
             cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
             constexpr int SW = TPW < 64 ? TPW : 64;
             constexpr int kNone = 0x7fffffff;
+            constexpr int RW = OUT == kOutTopKPhase ? 6 : 4;  // record width
+            auto xi = [](int k) { return kPhase ? pad16(k) : k; };
             __syncthreads();  // X row complete
             for (int s = 0; s < a.topk; ++s) {
                 T bp = T(-1);
                 int bb = kNone;
                 for (int b = a.kmin + t; b <= a.kmax; b += TPW) {
-                    const cpx<T> x = xrow[b];
+                    const cpx<T> x = xrow[xi(b)];
                     const T p = x.re * x.re + x.im * x.im;
                     if (p > bp || (p == bp && b < bb)) {
                         bp = p;
@@ -624,23 +717,36 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
                     bp = second ? p1 : p0;
                     bb = second ? b1 : b0;
                 }
-                T *rec = a.out + w * (int64_t)(4 * a.topk) + 4 * s;
+                T *rec = a.out + w * (int64_t)(RW * a.topk) + RW * s;
                 if (bb != kNone) {
                     if ((bb - a.kmin) % TPW == t) {
-                        const cpx<T> x = xrow[bb];
+                        const cpx<T> x = xrow[xi(bb)];
                         if (active) {
                             rec[0] = T(bb);
                             rec[1] = bp;
                             rec[2] = x.re;
                             rec[3] = x.im;
                         }
-                        xrow[bb] = {T(__builtin_nan("")), T(__builtin_nan(""))};
+                        xrow[xi(bb)] = {T(__builtin_nan("")), T(__builtin_nan(""))};
+                    }
+                    if constexpr (RW == 6) {  // phase fields from the owner of bin bb's chunk
+                        if ((bb >> 4) == t && active) {
+                            double ub = 0.0, gb = 0.0;
+#pragma unroll
+                            for (int j = 0; j < 16; ++j)
+                                if ((bb & 15) == j) {
+                                    ub = u[j];
+                                    gb = gd[j];
+                                }
+                            rec[4] = ub;
+                            rec[5] = gb;
+                        }
                     }
                 } else if (t == 0 && active) {  // fewer than k bins in range: (-1, -1) slots
                     rec[0] = T(-1);
                     rec[1] = T(-1);
-                    rec[2] = T(0);
-                    rec[3] = T(0);
+#pragma unroll
+                    for (int j = 2; j < RW; ++j) rec[j] = T(0);
                 }
                 if constexpr (TPW == 128) __syncthreads();  // retirement visible to both waves
             }

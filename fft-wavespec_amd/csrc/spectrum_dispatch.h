@@ -96,35 +96,48 @@ hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
     }
 }
 
-template <typename T, int LOG2N, int DETREND>
+// OSET selects the output modes one translation unit instantiates:
+// kSetBase = power / packed / top-k, kSetPhase = the fp64 phase outputs.
+enum OutSet : int { kSetBase = 0, kSetPhase = 1 };
+
+template <typename T, int LOG2N, int DETREND, int OSET>
 hipError_t dispatch_out(const SpectrumLaunch &L, hipStream_t s) {
-    switch (L.output) {
-    case kOutPacked: return dispatch_win<T, LOG2N, DETREND, kOutPacked>(L, s);
-    case kOutTopK: return dispatch_win<T, LOG2N, DETREND, kOutTopK>(L, s);
-    default: return dispatch_win<T, LOG2N, DETREND, kOutPower>(L, s);
+    if constexpr (OSET == kSetPhase) {
+        switch (L.output) {
+        case kOutPhase: return dispatch_win<T, LOG2N, DETREND, kOutPhase>(L, s);
+        case kOutTopKPhase: return dispatch_win<T, LOG2N, DETREND, kOutTopKPhase>(L, s);
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (L.output) {
+        case kOutPower: return dispatch_win<T, LOG2N, DETREND, kOutPower>(L, s);
+        case kOutPacked: return dispatch_win<T, LOG2N, DETREND, kOutPacked>(L, s);
+        case kOutTopK: return dispatch_win<T, LOG2N, DETREND, kOutTopK>(L, s);
+        default: return hipErrorInvalidValue;
+        }
     }
 }
 
-template <typename T, int LOG2N> hipError_t dispatch_detrend(const SpectrumLaunch &L, hipStream_t s) {
+template <typename T, int LOG2N, int OSET> hipError_t dispatch_detrend(const SpectrumLaunch &L, hipStream_t s) {
     switch (L.detrend) {
-    case kDetrendNone: return dispatch_out<T, LOG2N, kDetrendNone>(L, s);
-    case kDetrendMean: return dispatch_out<T, LOG2N, kDetrendMean>(L, s);
-    case kDetrendIir: return dispatch_out<T, LOG2N, kDetrendIir>(L, s);
+    case kDetrendNone: return dispatch_out<T, LOG2N, kDetrendNone, OSET>(L, s);
+    case kDetrendMean: return dispatch_out<T, LOG2N, kDetrendMean, OSET>(L, s);
+    case kDetrendIir: return dispatch_out<T, LOG2N, kDetrendIir, OSET>(L, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-template <typename T> hipError_t dispatch_n(const SpectrumLaunch &L, hipStream_t s) {
+template <typename T, int OSET = kSetBase> hipError_t dispatch_n(const SpectrumLaunch &L, hipStream_t s) {
     if (L.n_windows <= 0) return hipSuccess;
     switch (L.log2n) {
-    case 5: return dispatch_detrend<T, 5>(L, s);
-    case 6: return dispatch_detrend<T, 6>(L, s);
-    case 7: return dispatch_detrend<T, 7>(L, s);
-    case 8: return dispatch_detrend<T, 8>(L, s);
-    case 9: return dispatch_detrend<T, 9>(L, s);
-    case 10: return dispatch_detrend<T, 10>(L, s);
-    case 11: return dispatch_detrend<T, 11>(L, s);
-    case 12: return dispatch_detrend<T, 12>(L, s);
+    case 5: return dispatch_detrend<T, 5, OSET>(L, s);
+    case 6: return dispatch_detrend<T, 6, OSET>(L, s);
+    case 7: return dispatch_detrend<T, 7, OSET>(L, s);
+    case 8: return dispatch_detrend<T, 8, OSET>(L, s);
+    case 9: return dispatch_detrend<T, 9, OSET>(L, s);
+    case 10: return dispatch_detrend<T, 10, OSET>(L, s);
+    case 11: return dispatch_detrend<T, 11, OSET>(L, s);
+    case 12: return dispatch_detrend<T, 12, OSET>(L, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -5,7 +5,9 @@
 namespace wsp {
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream) {
-    return L.f32 ? launch_spectrum_f32(L, stream) : core::dispatch_n<double>(L, stream);
+    if (L.f32) return launch_spectrum_f32(L, stream);
+    if (L.output == kOutPhase || L.output == kOutTopKPhase) return launch_spectrum_phase(L, stream);
+    return core::dispatch_n<double>(L, stream);
 }
 
 }  // namespace wsp

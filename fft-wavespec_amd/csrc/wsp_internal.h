@@ -14,7 +14,7 @@ constexpr int kMaxLog2N = 12;  // N = 4096
 constexpr int kBlock = 128;    // threads per workgroup (2 waves)
 
 enum Detrend : int { kDetrendNone = 0, kDetrendMean = 1, kDetrendIir = 2, kDetrendKalman = 3 };
-enum Output : int { kOutPower = 0, kOutPacked = 1, kOutTopK = 2 };
+enum Output : int { kOutPower = 0, kOutPacked = 1, kOutTopK = 2, kOutPhase = 3, kOutTopKPhase = 4 };
 
 // Everything a spectrum launch needs; pointer types are erased so one
 // struct serves the f64 and f32 instantiations.
@@ -41,6 +41,25 @@ struct SpectrumLaunch {
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);
 hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t stream);
+hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t stream);  // kOutPhase, kOutTopKPhase (f64)
+
+// Inverse real FFT of packed spectra (gpu_fft_real_inverse,
+// L/WaveSpecZZ_1.0.4-core.mq5:65,426): n_windows rows of N doubles in the
+// gpu_fft_real_forward layout -> n_windows rows of N samples.
+struct InverseLaunch {
+    const double *in;
+    double *out;
+    const void *twiddle;  // N complex W_N^k (double)
+    int64_t n_windows;
+    int log2n;
+    int grid;             // 0 = auto
+};
+hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream);
+
+// Phase / unwrap / group delay of one packed spectrum of n_bins bins
+// (gpu_spectral_phase_unwrap, L/WaveSpecZZ_1.0.4-core.mq5:72,416):
+// method 0 unwrapped phase, 1 wrapped phase, 2 group delay; out[n_bins].
+hipError_t launch_phase_row(const double *spec, int n_bins, int method, double *out, hipStream_t stream);
 
 // Per-window Kalman 4D detrend pre-pass: d[w*N + j] = x_j - trend_j
 // (one lane per window; trend arithmetic in fp64 like the MQL5 source).

@@ -24,7 +24,8 @@ STATUS_NAMES = {OK: "OK", BAD_ARGS: "BAD_ARGS", BACKEND_UNAVAILABLE: "BACKEND_UN
 DETREND = {"none": 0, "mean": 1, "iir": 2, "kalman": 3}
 WINDOW = {"none": 0, "hann": 1, "hamming": 2, "blackman": 3, "bartlett": 4}
 PRECISION = {"f64": 0, "f32": 1}
-OUTPUT = {"power": 0, "packed": 1, "topk": 2}
+OUTPUT = {"power": 0, "packed": 1, "topk": 2, "phase": 3, "topk_phase": 4}
+PHASE_METHOD = {"unwrapped": 0, "wrapped": 1, "group_delay": 2}
 
 _d = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)
@@ -46,6 +47,12 @@ SIGNATURES = {
     "gpu_free_job": (C.c_int32, [C.c_int64]),
     "gpu_get_last_error_w": (C.c_int32, [C.POINTER(C.c_uint16), C.c_int32]),
     "gpu_fft_real_forward_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, _d]),
+    "gpu_fft_real_inverse": (C.c_int32, [_d, C.c_int32, _d]),
+    "gpu_fft_real_inverse_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, _d]),
+    "gpu_spectral_phase_unwrap": (C.c_int32, [_d, C.c_int32, C.c_int32, _d, C.c_int32]),
+    "gpu_spectrum_topk_phase_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                                  C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32,
+                                                  _i32p]),
     "gpu_spectrum_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_int32, C.c_int32, _d, C.c_int32, _i32p]),
     "gpu_submit_spectrum_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
@@ -57,6 +64,7 @@ SIGNATURES = {
     "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
+    "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
     "wsp_plan_execute": (C.c_int32, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "wsp_plan_algorithmic_bytes": (C.c_int64, [C.c_int64]),
     "wsp_plan_destroy": (C.c_int32, [C.c_int64]),
@@ -130,13 +138,43 @@ def fft_real_forward_batch(windows: np.ndarray) -> np.ndarray:
     return out
 
 
+def fft_real_inverse(spec: np.ndarray) -> np.ndarray:
+    """gpu_fft_real_inverse: packed spectrum (gpu_fft_real_forward layout) -> samples."""
+    spec = np.ascontiguousarray(spec, dtype=np.float64)
+    out = np.empty_like(spec)
+    _check("gpu_fft_real_inverse", lib().gpu_fft_real_inverse(_dptr(spec), spec.size, _dptr(out)))
+    return out
+
+
+def fft_real_inverse_batch(spectra: np.ndarray) -> np.ndarray:
+    s = np.ascontiguousarray(spectra, dtype=np.float64)
+    out = np.empty_like(s)
+    _check("gpu_fft_real_inverse_batch",
+           lib().gpu_fft_real_inverse_batch(_dptr(s), s.shape[1], s.shape[0], _dptr(out)))
+    return out
+
+
+def spectral_phase_unwrap(spec: np.ndarray, method="unwrapped") -> np.ndarray:
+    """gpu_spectral_phase_unwrap over a packed spectrum -> spectrum_len/2 values."""
+    spec = np.ascontiguousarray(spec, dtype=np.float64)
+    out = np.empty(spec.size // 2)
+    _check("gpu_spectral_phase_unwrap",
+           lib().gpu_spectral_phase_unwrap(_dptr(spec), spec.size, PHASE_METHOD[method], _dptr(out), out.size))
+    return out
+
+
+def _record(window_len: int, output: str, top_k: int = 8) -> int:
+    return {"packed": window_len, "topk": 4 * top_k, "topk_phase": 6 * top_k,
+            "phase": 3 * (window_len // 2)}.get(output, window_len // 2)
+
+
 def spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
                    trend_period: int = 0, precision="f64", output="power", max_records: int | None = None
                    ) -> np.ndarray:
     """gpu_spectrum_batch over a chronological series -> (nwin, record) array."""
     s = np.ascontiguousarray(series, dtype=np.float64)
     nwin = 1 + (s.size - window_len) // hop
-    rec = window_len if OUTPUT[output] == 1 else window_len // 2
+    rec = _record(window_len, output)
     if max_records is not None:
         nwin = min(nwin, max_records)
     out = np.empty((nwin, rec), dtype=np.float64)
@@ -160,6 +198,21 @@ def spectrum_topk_batch(series: np.ndarray, window_len: int, hop: int, detrend="
            lib().gpu_spectrum_topk_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
                                          trend_period, PRECISION[precision], top_k, min_period, max_period,
                                          _dptr(out), out.size, C.byref(n_out)))
+    return out[: n_out.value]
+
+
+def spectrum_topk_phase_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
+                              trend_period: int = 0, top_k: int = 8, min_period: float = 18.0,
+                              max_period: float = 200.0) -> np.ndarray:
+    """gpu_spectrum_topk_phase_batch -> (nwin, top_k, 6) [bin, power, Re, Im, phase, group delay]."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - window_len) // hop
+    out = np.empty((nwin, top_k, 6), dtype=np.float64)
+    n_out = C.c_int32(0)
+    _check("gpu_spectrum_topk_phase_batch",
+           lib().gpu_spectrum_topk_phase_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
+                                               trend_period, top_k, min_period, max_period, _dptr(out), out.size,
+                                               C.byref(n_out)))
     return out[: n_out.value]
 
 
@@ -200,12 +253,26 @@ class Plan:
         if self.handle == 0:
             raise BridgeError("wsp_plan_create", INTERNAL_ERROR, last_error())
         self.window_len, self.hop, self.n_windows = window_len, hop, n_windows
-        self.record = window_len if OUTPUT[output] == 1 else window_len // 2
+        self.output = output
+        self.record = _record(window_len, output)
         self.series_len = (n_windows - 1) * hop + window_len
+
+    @classmethod
+    def inverse(cls, device: int, window_len: int, n_windows: int) -> "Plan":
+        """wsp_plan_create_inverse: rows of packed spectra -> rows of samples."""
+        self = cls.__new__(cls)
+        self.handle = lib().wsp_plan_create_inverse(device, window_len, n_windows)
+        if self.handle == 0:
+            raise BridgeError("wsp_plan_create_inverse", INTERNAL_ERROR, last_error())
+        self.window_len, self.hop, self.n_windows = window_len, window_len, n_windows
+        self.output = "inverse"
+        self.record = window_len
+        self.series_len = n_windows * window_len
+        return self
 
     def set_topk(self, top_k: int, min_period: float, max_period: float) -> None:
         _check("wsp_plan_set_topk", lib().wsp_plan_set_topk(self.handle, top_k, min_period, max_period))
-        self.record = 4 * top_k
+        self.record = (6 if self.output == "topk_phase" else 4) * top_k
 
     @property
     def algorithmic_bytes(self) -> int:

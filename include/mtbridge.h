@@ -61,6 +61,16 @@ extern "C" {
  * bins in [ceil(N/max_period), floor(N/min_period)] clamped to N/2-1, empty slots
  * [-1, -1, 0, 0]. */
 #define MTB_OUT_TOPK 2
+/* phase outputs (fp64 only), CalculateFFTPhase / UnwrapPhase /
+ * CalculateGroupDelay of L/WaveSpecZZ_1.0.4-new.mq5:1040-1120 run at :3225-3227
+ * over n = N entries (X_k for k < N/2, zero above: the GPU unpack :3183-3196):
+ *   MTB_OUT_PHASE      record of 3*(N/2) doubles [P_k | unwrapped phase_k |
+ *                      group delay_k (clamped to +-100)], k < N/2;
+ *   MTB_OUT_TOPK_PHASE top_k slots of [bin, power, Re, Im, unwrapped phase,
+ *                      group delay] (the values the ETA estimators read at the
+ *                      dominant bin, :1165 and :1239); empty [-1, -1, 0, 0, 0, 0]. */
+#define MTB_OUT_PHASE 3
+#define MTB_OUT_TOPK_PHASE 4
 
 /* =====================================================================
  * 1. Reference surface -- Include/imports.mqh:5-19 (exact signatures)
@@ -121,6 +131,30 @@ MTB_API int32_t gpu_get_last_error_w(uint16_t *buf, int32_t buf_len);
  * gpu_fft_real_forward. */
 MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len, int32_t n_windows, double *out);
 
+/* Inverse of gpu_fft_real_forward (declared L/WaveSpecZZ_1.0.4-core.mq5:65;
+ * called at :426 on the forward output of :344 after the spectral stages, the
+ * result goes back into the time-domain pipeline at :432).  The DLL's own
+ * numerics are unpinned (no CPU counterpart in the reference); defined here
+ * as the exact inverse of the packed layout: in[2k] + i in[2k+1] = X_k for
+ * 0 < k < len/2, X_0 = in[0] (in[1], Im X_0 of a real signal, is ignored),
+ * X_{len/2} = 0 (no slot in the layout), out[n] = (1/len) sum_k X_k
+ * e^{+2 pi i k n/len}.  inverse(forward(x)) == x for x without a Nyquist
+ * component.  len: power of two, 32..4096.  Synchronous. */
+MTB_API int32_t gpu_fft_real_inverse(const double *in_spec, int32_t len, double *out);
+
+/* Batch form: n_windows packed spectra in[w*window_len ...] -> samples. */
+MTB_API int32_t gpu_fft_real_inverse_batch(const double *in, int32_t window_len, int32_t n_windows, double *out);
+
+/* L/WaveSpecZZ_1.0.4-core.mq5:72 (called at :416 on the packed forward
+ * output).  spectrum: spectrum_len doubles = spectrum_len/2 packed bins (any
+ * even length >= 2); bins from spectrum_len/2 up are the zeroed upper half of
+ * the reference's arrays.  method 0: unwrapped phase, 1: wrapped phase
+ * atan2(Im, Re), 2: group delay (clamped +-100); out[k] for k <
+ * spectrum_len/2 (out_len >= spectrum_len/2).  Method numbering is
+ * build-defined (the DLL is unpinned).  Synchronous. */
+MTB_API int32_t gpu_spectral_phase_unwrap(const double *spectrum, int32_t spectrum_len, int32_t method, double *out,
+                                          int32_t out_len);
+
 /* =====================================================================
  * 3. Hot path: batched sliding-window power spectrum over a series
  *    (shape of gpu_submit_extract_cycles_batch, imports.mqh:14-16;
@@ -159,6 +193,13 @@ MTB_API int32_t gpu_spectrum_topk_batch(const double *series, int32_t series_len
                                         int32_t top_k, double min_period, double max_period, double *out,
                                         int32_t out_cap, int32_t *out_len);
 
+/* gpu_spectrum_topk_batch with MTB_OUT_TOPK_PHASE records (6*top_k doubles
+ * per window: bin, power, Re, Im, unwrapped phase, group delay).  fp64. */
+MTB_API int32_t gpu_spectrum_topk_phase_batch(const double *series, int32_t series_len, int32_t window_len,
+                                              int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
+                                              int32_t top_k, double min_period, double max_period, double *out,
+                                              int32_t out_cap, int32_t *out_len);
+
 /* Kalman 4D parameters for MTB_DETREND_KALMAN, in the order of the inputs
  * at L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901: follow_strength,
  * q_pos, q_vel, q_acc, q_jerk, adapt_gain, meas_noise, init_var_pos,
@@ -178,13 +219,19 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
                                 int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
                                 int32_t output);
 
+/* Device-resident inverse plan (gpu_fft_real_inverse_batch on HBM buffers):
+ * wsp_plan_execute reads n_windows packed spectra of window_len doubles and
+ * writes n_windows rows of window_len samples. */
+MTB_API int64_t wsp_plan_create_inverse(int32_t device, int32_t window_len, int64_t n_windows);
+
 /* Enqueues the hot path on `hip_stream` (a hipStream_t; NULL = the null
  * stream) reading d_series (device pointer, double or float per the plan's
  * precision, >= (n_windows-1)*hop + window_len elements) and writing d_out
  * (n_windows * record elements).  Asynchronous; no allocation, no sync. */
 MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream);
 
-/* Switches a plan to MTB_OUT_TOPK records (4*top_k elements per window). */
+/* Sets a top-k plan's scan: MTB_OUT_TOPK (4*top_k elements per window; a
+ * power/packed plan switches to it) or MTB_OUT_TOPK_PHASE (6*top_k). */
 MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period);
 
 /* Bytes the plan's algorithm must move per execute: unique input samples

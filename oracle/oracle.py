@@ -51,6 +51,13 @@ def lib() -> C.CDLL:
         h.ora_batch_topk.argtypes = [_d, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, _d, C.c_int,
                                      C.c_double, C.c_double, _d]
         h.ora_batch_topk.restype = C.c_int64
+        h.ora_fft_real_inverse.argtypes = [_d, C.c_int, _d]
+        h.ora_phase_unwrap.argtypes = [_d, _d, C.c_int, _d, _d, _d]
+        h.ora_batch_phase.argtypes = [_d, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, _d, _d]
+        h.ora_batch_phase.restype = C.c_int64
+        h.ora_batch_topk_phase.argtypes = [_d, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, _d, C.c_int,
+                                           C.c_double, C.c_double, _d]
+        h.ora_batch_topk_phase.restype = C.c_int64
         _lib = h
     return _lib
 
@@ -104,6 +111,48 @@ def batch_topk(series, n, hop, detrend="none", window="hann", trend_period=0, ka
     kp = np.ascontiguousarray(KALMAN_DEFAULTS if kalman is None else kalman, dtype=np.float64)
     got = lib().ora_batch_topk(_p(s), s.size, n, hop, DETREND[detrend], WINDOW[window], trend_period, _p(kp), top_k,
                                min_period, max_period, _p(out))
+    assert got == nwin
+    return out
+
+
+def fft_real_inverse(packed) -> np.ndarray:
+    """Build-defined inverse of the packed forward layout (wavespec_oracle.c ora_fft_real_inverse)."""
+    p = np.ascontiguousarray(packed, dtype=np.float64)
+    out = np.empty_like(p)
+    lib().ora_fft_real_inverse(_p(p), p.size, _p(out))
+    return out
+
+
+def phase_unwrap(packed) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(wrapped, unwrapped, group delay) for k < len/2 of a packed spectrum (1.0.4-new.mq5:1040-1120)."""
+    p = np.ascontiguousarray(packed, dtype=np.float64)
+    re, im = np.ascontiguousarray(p[0::2]), np.ascontiguousarray(p[1::2])
+    h = p.size // 2
+    ph, u, gd = np.empty(h), np.empty(h), np.empty(h)
+    lib().ora_phase_unwrap(_p(re), _p(im), p.size, _p(ph), _p(u), _p(gd))
+    return ph, u, gd
+
+
+def batch_phase(series, n, hop, detrend="none", window="hann", trend_period=0, kalman=None) -> np.ndarray:
+    """(nwin, 3, N/2): [power, unwrapped phase, group delay] per window (MTB_OUT_PHASE)."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - n) // hop
+    out = np.empty((nwin, 3, n // 2))
+    kp = np.ascontiguousarray(KALMAN_DEFAULTS if kalman is None else kalman, dtype=np.float64)
+    got = lib().ora_batch_phase(_p(s), s.size, n, hop, DETREND[detrend], WINDOW[window], trend_period, _p(kp), _p(out))
+    assert got == nwin
+    return out
+
+
+def batch_topk_phase(series, n, hop, detrend="none", window="hann", trend_period=0, kalman=None, top_k=8,
+                     min_period=18.0, max_period=200.0) -> np.ndarray:
+    """(nwin, top_k, 6): [bin, power, Re, Im, unwrapped phase, group delay] (MTB_OUT_TOPK_PHASE)."""
+    s = np.ascontiguousarray(series, dtype=np.float64)
+    nwin = 1 + (s.size - n) // hop
+    out = np.empty((nwin, top_k, 6))
+    kp = np.ascontiguousarray(KALMAN_DEFAULTS if kalman is None else kalman, dtype=np.float64)
+    got = lib().ora_batch_topk_phase(_p(s), s.size, n, hop, DETREND[detrend], WINDOW[window], trend_period, _p(kp),
+                                     top_k, min_period, max_period, _p(out))
     assert got == nwin
     return out
 

@@ -347,6 +347,109 @@ ORA_EXPORT void ora_topk_bins(const double *re, const double *im, int n, int top
     }
 }
 
+/* ------------------------------------------------------ inverse real FFT */
+
+/* Complex radix-2 DIT with FourierTransformManual's structure
+ * (L/WaveSpecZZ_1.0.2.mq5:938-974) on a complex input: bit reversal, then
+ * butterflies with the twiddle recurrence and sign -2*pi/len. */
+static void cfft_manual(double *re, double *im, int n) {
+    for (int i = 1, j = 0; i < n; i++) {
+        int bit = n >> 1;
+        for (; (j & bit) != 0; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            double t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    for (int len = 2; len <= n; len <<= 1) {
+        double ang = -2 * M_PI / len;
+        double wlen_real = cos(ang), wlen_imag = sin(ang);
+        for (int i = 0; i < n; i += len) {
+            double w_real = 1.0, w_imag = 0.0;
+            for (int j = 0; j < len / 2; j++) {
+                int idx1 = i + j, idx2 = i + j + len / 2;
+                double t_real = re[idx2] * w_real - im[idx2] * w_imag;
+                double t_imag = re[idx2] * w_imag + im[idx2] * w_real;
+                re[idx2] = re[idx1] - t_real;
+                im[idx2] = im[idx1] - t_imag;
+                re[idx1] += t_real;
+                im[idx1] += t_imag;
+                double w_temp = w_real;
+                w_real = w_real * wlen_real - w_imag * wlen_imag;
+                w_imag = w_temp * wlen_imag + w_imag * wlen_real;
+            }
+        }
+    }
+}
+
+/* gpu_fft_real_inverse (declared L/WaveSpecZZ_1.0.4-core.mq5:65; called at
+ * :426 on the output of gpu_fft_real_forward :344 after the spectral stages,
+ * result copied back into the time-domain pipeline :432).  DLL-only, no CPU
+ * counterpart in the reference, so BUILD-DEFINED as the exact inverse of the
+ * packed forward layout: X_k = in[2k] + i in[2k+1] for 0 < k < N/2,
+ * X_0 = in[0] (a real signal's Im X_0 is 0: in[1] is ignored), X_{N/2} = 0
+ * (the layout has no slot for it), X_{N-k} = conj X_k, and
+ * x_n = (1/N) sum_k X_k e^{+2 pi i k n/N} = conj(DFT(conj X))_n / N. */
+ORA_EXPORT void ora_fft_real_inverse(const double *in, int n, double *out) {
+    if (n < 2) { if (n == 1) out[0] = in[0]; return; }
+    double *re = (double *)malloc(sizeof(double) * (size_t)n);
+    double *im = (double *)malloc(sizeof(double) * (size_t)n);
+    const int h = n / 2;
+    for (int k = 0; k < n; k++) { /* conj X_k */
+        if (k == 0) { re[k] = in[0]; im[k] = 0.0; }
+        else if (k < h) { re[k] = in[2 * k]; im[k] = -in[2 * k + 1]; }
+        else if (k == h) { re[k] = 0.0; im[k] = 0.0; }
+        else { re[k] = in[2 * (n - k)]; im[k] = in[2 * (n - k) + 1]; }
+    }
+    cfft_manual(re, im, n);
+    for (int i = 0; i < n; i++) out[i] = re[i] / (double)n;
+    free(re); free(im);
+}
+
+/* -------------------------------------------------- phase / unwrap / delay */
+
+/* CalculateFFTPhase + UnwrapPhase + CalculateGroupDelay,
+ * L/WaveSpecZZ_1.0.4-new.mq5:1040-1120 (same as L/WaveSpecZZ_1.0.2.mq5:980-1060),
+ * called at :3225-3227 with n = InpFFTWindow over fft_real/fft_imag as the GPU
+ * unpack path leaves them (:3183-3196): X_k for k < N/2, zero above.
+ * Same expression order as the MQL5 source (sequential unwrap).  Writes the
+ * first N/2 entries of each requested array (NULL skips it). */
+ORA_EXPORT void ora_phase_unwrap(const double *re, const double *im, int n, double *phase_out,
+                                 double *unwrapped_out, double *gd_out) {
+    if (n < 2) return;
+    double *ph = (double *)malloc(sizeof(double) * (size_t)n);
+    double *u = (double *)malloc(sizeof(double) * (size_t)n);
+    double *gd = (double *)malloc(sizeof(double) * (size_t)n);
+    for (int i = 0; i < n; i++) /* :1046-1049; upper half zero -> atan2(0, 0) = 0 */
+        ph[i] = i < n / 2 ? atan2(im[i], re[i]) : atan2(0.0, 0.0);
+    u[0] = ph[0]; /* :1063 */
+    for (int i = 1; i < n; i++) { /* :1066-1080 */
+        double diff = ph[i] - ph[i - 1];
+        double correction = 0;
+        if (diff > M_PI) correction = -2.0 * M_PI;
+        else if (diff < -M_PI) correction = 2.0 * M_PI;
+        u[i] = u[i - 1] + diff + correction;
+    }
+    if (n < 3) { /* :1092-1096 */
+        for (int i = 0; i < n; i++) gd[i] = 0.0;
+    } else {
+        gd[0] = -(u[1] - u[0]); /* :1102 */
+        for (int i = 1; i < n - 1; i++) gd[i] = -(u[i + 1] - u[i - 1]) / 2.0; /* :1105-1108 */
+        gd[n - 1] = -(u[n - 1] - u[n - 2]); /* :1111 */
+        for (int i = 0; i < n; i++) { /* :1115-1119 */
+            if (gd[i] > 100.0) gd[i] = 100.0;
+            if (gd[i] < -100.0) gd[i] = -100.0;
+        }
+    }
+    for (int k = 0; k < n / 2; k++) {
+        if (phase_out) phase_out[k] = ph[k];
+        if (unwrapped_out) unwrapped_out[k] = u[k];
+        if (gd_out) gd_out[k] = gd[k];
+    }
+    free(ph); free(u); free(gd);
+}
+
 /* ---------------------------------------------------------- full pipeline */
 
 static int is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
@@ -413,5 +516,62 @@ ORA_EXPORT int64_t ora_batch_spectrum(const double *series, int64_t series_len, 
     for (int64_t w = 0; w < nwin; w++)
         ora_window_spectrum(series + w * hop, n, detrend, window, trend_period, kalman16, output,
                             out + w * stride);
+    return nwin;
+}
+
+/* MTB_OUT_PHASE records for every window: [P_k | unwrapped phase_k |
+ * group delay_k], k < N/2 (3N/2 doubles per window). */
+ORA_EXPORT int64_t ora_batch_phase(const double *series, int64_t series_len, int n, int64_t hop, int detrend,
+                                   int window, int trend_period, const double *kalman16, double *out) {
+    if (!is_pow2(n) || hop <= 0 || series_len < n) return -1;
+    int64_t nwin = 1 + (series_len - n) / hop;
+    const int h = n / 2;
+#pragma omp parallel for schedule(static)
+    for (int64_t w = 0; w < nwin; w++) {
+        double *packed = (double *)malloc(sizeof(double) * (size_t)n);
+        double *re = (double *)malloc(sizeof(double) * (size_t)h);
+        double *im = (double *)malloc(sizeof(double) * (size_t)h);
+        double *rec = out + w * 3 * (int64_t)h;
+        ora_window_spectrum(series + w * hop, n, detrend, window, trend_period, kalman16, 1, packed);
+        for (int k = 0; k < h; k++) { re[k] = packed[2 * k]; im[k] = packed[2 * k + 1]; }
+        ora_power(re, im, n, rec);
+        ora_phase_unwrap(re, im, n, NULL, rec + h, rec + 2 * h);
+        free(packed); free(re); free(im);
+    }
+    return nwin;
+}
+
+/* MTB_OUT_TOPK_PHASE records: the top-k scan (ora_topk_bins) plus the
+ * unwrapped phase and group delay of each chosen bin -- the values the ETA
+ * estimators read at the dominant bin (L/WaveSpecZZ_1.0.4-new.mq5:1165, :1239)
+ * -- 6 doubles per slot [bin, power, Re, Im, phase, delay]; empty slots
+ * [-1, -1, 0, 0, 0, 0]. */
+ORA_EXPORT int64_t ora_batch_topk_phase(const double *series, int64_t series_len, int n, int64_t hop, int detrend,
+                                        int window, int trend_period, const double *kalman16, int top_k,
+                                        double min_period, double max_period, double *out) {
+    if (!is_pow2(n) || hop <= 0 || series_len < n || top_k < 1 || top_k > 64) return -1;
+    int64_t nwin = 1 + (series_len - n) / hop;
+    const int h = n / 2;
+#pragma omp parallel for schedule(static)
+    for (int64_t w = 0; w < nwin; w++) {
+        double *packed = (double *)malloc(sizeof(double) * (size_t)n);
+        double *re = (double *)malloc(sizeof(double) * (size_t)h);
+        double *im = (double *)malloc(sizeof(double) * (size_t)h);
+        double *u = (double *)malloc(sizeof(double) * (size_t)h);
+        double *gd = (double *)malloc(sizeof(double) * (size_t)h);
+        double rec4[4 * 64];
+        ora_window_spectrum(series + w * hop, n, detrend, window, trend_period, kalman16, 1, packed);
+        for (int k = 0; k < h; k++) { re[k] = packed[2 * k]; im[k] = packed[2 * k + 1]; }
+        ora_topk_bins(re, im, n, top_k, min_period, max_period, rec4);
+        ora_phase_unwrap(re, im, n, NULL, u, gd);
+        double *rec = out + w * 6 * (int64_t)top_k;
+        for (int s = 0; s < top_k; s++) {
+            const int b = (int)rec4[4 * s];
+            for (int j = 0; j < 4; j++) rec[6 * s + j] = rec4[4 * s + j];
+            rec[6 * s + 4] = b >= 0 ? u[b] : 0.0;
+            rec[6 * s + 5] = b >= 0 ? gd[b] : 0.0;
+        }
+        free(packed); free(re); free(im); free(u); free(gd);
+    }
     return nwin;
 }

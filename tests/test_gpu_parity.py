@@ -280,3 +280,159 @@ def test_topk_f32_and_plan(gpu_session):
     _topk_match(d_o.cpu().numpy().reshape(w, 8, 4), oracle.batch_topk(s, n, n, "none", "hann", 0, None, 8, 18, 200),
                 1e-10, ref(s, n, n).max(axis=1))
     plan.close()
+
+
+# ---------------------------------------------------------------- inverse + phase
+def _nyquist_free(x):
+    n = x.shape[-1]
+    alt = (-1.0) ** np.arange(n)
+    return x - np.outer(x @ alt, alt).reshape(x.shape) / n
+
+
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+def test_inverse_batch_vs_oracle(gpu_session, n):
+    """gpu_fft_real_inverse_batch (L/WaveSpecZZ_1.0.4-core.mq5:65,426) on random packed spectra,
+    ragged window count; bar: max |x - x_ref| <= 1e-12 * max |x_ref| (fp64 round-off of two FFTs)."""
+    rng = np.random.default_rng(n)
+    w = 37
+    spec = rng.standard_normal((w, n))
+    got = bridge.fft_real_inverse_batch(spec)
+    for i in range(w):
+        want = oracle.fft_real_inverse(spec[i])
+        assert np.max(np.abs(got[i] - want)) <= 1e-12 * np.max(np.abs(want)), i
+
+
+@pytest.mark.parametrize("n", [32, 1024, 4096])
+def test_inverse_round_trip_single(gpu_session, n):
+    """gpu_fft_real_inverse(gpu_fft_real_forward(x)) == x (x without a Nyquist component), the
+    round trip ApplySpectralStages makes (core.mq5:344 -> :426)."""
+    x = _nyquist_free(synth.random_walk(n, n))
+    back = bridge.fft_real_inverse(bridge.fft_real_forward(x))
+    assert np.max(np.abs(back - x)) <= 1e-13 * np.max(np.abs(x))
+
+
+def test_inverse_plan_full_size(gpu_session):
+    """Device-resident forward (packed) -> inverse plans over 65536 x 4096 fp64 (2 GiB each way):
+    round trip returns x minus its Nyquist component for every window."""
+    torch = pytest.importorskip("torch")
+    n, w = 4096, 65536
+    dev = torch.device("cuda", 0)
+    d_x = synth.random_walk_torch(n * w, 5, dev)
+    d_spec = torch.empty(w * n, dtype=torch.float64, device=dev)
+    d_back = torch.empty(w * n, dtype=torch.float64, device=dev)
+    fwd = bridge.Plan(0, n, n, w, "none", "none", output="packed")
+    inv = bridge.Plan.inverse(0, n, w)
+    assert inv.algorithmic_bytes == 2 * n * w * 8
+    stream = torch.cuda.current_stream().cuda_stream
+    fwd.execute(d_x.data_ptr(), d_spec.data_ptr(), stream)
+    inv.execute(d_spec.data_ptr(), d_back.data_ptr(), stream)
+    torch.cuda.synchronize()
+    X, Y = d_x.view(w, n), d_back.view(w, n)
+    alt = torch.ones(n, dtype=torch.float64, device=dev)
+    alt[1::2] = -1.0
+    want = X - (X @ alt)[:, None] * alt[None, :] / n
+    err = ((Y - want).abs().amax(dim=1) / want.abs().amax(dim=1)).max().item()
+    assert err <= 1e-13
+    fwd.close()
+    inv.close()
+
+
+def _phase_tol(mag, rel=1e-10):
+    """A phase computed from X_k carries |dX| / |X_k| of error: with |dX| ~ 1e-13 max |X| (the
+    spectra's own fp64 parity), bar = rel * max|X| / |X_k| (1000x margin), never below rel."""
+    return rel * np.maximum(mag.max() / np.maximum(mag, 1e-300), 1.0)
+
+
+def _unwrap_match(got, want, mag):
+    """Unwrapped phases agree within _phase_tol on well-conditioned bins (|X_k| >= 1e-9 max |X|);
+    a 2 pi offset is allowed only after an ill-conditioned bin, whose phase is rounding noise and
+    whose jump decision therefore is too (e.g. X_0 of a mean-removed window)."""
+    ok = mag >= 1e-9 * mag.max()
+    d = got - want
+    m = np.round(d / (2 * np.pi))
+    assert np.all((np.abs(d - 2 * np.pi * m) <= _phase_tol(mag))[ok])
+    steps = np.nonzero(np.diff(m) != 0)[0] + 1
+    for k in steps:
+        assert not (ok[k] and ok[k - 1]), k
+    return m
+
+
+def _delay_match(got, want, mag, m):
+    """Group delay = differences of neighbouring unwrapped phases: bar from the worse neighbour."""
+    ok = mag >= 1e-9 * mag.max()
+    tol = _phase_tol(mag)
+    tn = tol.copy()
+    tn[1:] = np.maximum(tn[1:], tol[:-1])
+    tn[:-1] = np.maximum(tn[:-1], tol[1:])
+    cond = ok.copy()
+    cond[1:-1] &= ok[:-2] & ok[2:] & (m[:-2] == m[2:])
+    assert np.all((np.abs(got - want) <= tn)[cond])
+
+
+@pytest.mark.parametrize("n", [32, 256, 1024, 4096])
+@pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024)])
+def test_phase_output(gpu_session, n, detrend, period):
+    """MTB_OUT_PHASE: [P | unwrapped phase | group delay] (1.0.4-new.mq5:1040-1120 at :3225-3227)."""
+    hop = n // 2 + 3
+    s = synth.random_walk(24 * hop + n, seed=n + 3)
+    got = gpu(s, n, hop, detrend, "hann", period, output="phase")
+    nwin = got.shape[0]
+    got = got.reshape(nwin, 3, n // 2)
+    want = oracle.batch_phase(s, n, hop, detrend, "hann", period)
+    assert oracle.rel_err(got[:, 0], want[:, 0]) <= 1e-10
+    for w in range(nwin):
+        mag = np.sqrt(want[w, 0])
+        m = _unwrap_match(got[w, 1], want[w, 1], mag)
+        _delay_match(got[w, 2], want[w, 2], mag, m)
+
+
+@pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64)])
+def test_topk_phase(gpu_session, n, hop, k, minp, maxp):
+    """MTB_OUT_TOPK_PHASE: top-k records + unwrapped phase / group delay at each chosen bin (the
+    values ComputeETA_RealFFT / CalculateScientificETASeconds read, 1.0.4-new.mq5:1165, :1239)."""
+    s = synth.random_walk((30 - 1) * hop + n, seed=n + k + 1)
+    got = bridge.spectrum_topk_phase_batch(s, n, hop, "iir", "hann", 1024, k, minp, maxp)
+    want = oracle.batch_topk_phase(s, n, hop, "iir", "hann", 1024, None, k, minp, maxp)
+    _topk_match(got[:, :, :4], want[:, :, :4], 1e-10, ref(s, n, hop, "iir", "hann", 1024).max(axis=1))
+    full = oracle.batch_phase(s, n, hop, "iir", "hann", 1024)
+    for w in range(got.shape[0]):
+        mag = np.sqrt(full[w, 0])
+        ok = mag >= 1e-9 * mag.max()
+        same = (got[w, :, 0] == want[w, :, 0]) & (want[w, :, 0] >= 0)
+        b = want[w, same, 0].astype(int)
+        if ok[: max(b.max(initial=0), 1) + 2].all():  # no ill-conditioned bin up to the chosen ones
+            assert np.max(np.abs(got[w, same, 4:] - want[w, same, 4:]), initial=0.0) <= 1e-8
+
+
+@pytest.mark.parametrize("length", [2, 6, 64, 1000, 4096, 10002])
+@pytest.mark.parametrize("method", ["unwrapped", "wrapped", "group_delay"])
+def test_spectral_phase_unwrap(gpu_session, length, method):
+    """gpu_spectral_phase_unwrap (L/WaveSpecZZ_1.0.4-core.mq5:72,416) on packed spectra of any even
+    length (incl. non-powers of two, as after gpu_spectral_upscale)."""
+    rng = np.random.default_rng(length)
+    spec = rng.standard_normal(length)
+    got = bridge.spectral_phase_unwrap(spec, method)
+    ph, u, gd = oracle.phase_unwrap(spec)
+    want = {"unwrapped": u, "wrapped": ph, "group_delay": gd}[method]
+    assert got.shape == want.shape
+    assert np.max(np.abs(got - want)) <= 1e-9
+
+
+def test_phase_plan_and_bad_precision(gpu_session):
+    torch = pytest.importorskip("torch")
+    n, w = 2048, 200
+    s = synth.random_walk(n * w, seed=8)
+    plan = bridge.Plan(0, n, n, w, "none", "blackman", output="phase")
+    d_s = torch.from_numpy(s).cuda()
+    d_o = torch.empty(w * 3 * (n // 2), dtype=torch.float64, device="cuda")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_o.cpu().numpy().reshape(w, 3, n // 2)
+    want = oracle.batch_phase(s, n, n, "none", "blackman")
+    assert oracle.rel_err(got[:, 0], want[:, 0]) <= 1e-10
+    for i in (0, w // 2, w - 1):
+        m = _unwrap_match(got[i, 1], want[i, 1], np.sqrt(want[i, 0]))
+        _delay_match(got[i, 2], want[i, 2], np.sqrt(want[i, 0]), m)
+    plan.close()
+    with pytest.raises(bridge.BridgeError):
+        bridge.spectrum_batch(s[: 4 * n], n, n, "none", "hann", 0, "f32", "phase")

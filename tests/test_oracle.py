@@ -121,3 +121,72 @@ def test_golden_vectors(path):
     assert np.array_equal(p, g["power"])
     q = oracle.batch_spectrum(*args, kalman=g["kalman"], output="packed")
     assert np.array_equal(q, g["packed"])
+
+
+# ---------------------------------------------------------------- top-k, inverse, phase
+def test_topk_bins_vs_numpy_sort():
+    """ora_topk_bins' insertion scan == a stable sort by (power desc, bin asc) over the period range."""
+    n, k = 1024, 8
+    s = synth.random_walk(30 * n, 21)
+    got = oracle.batch_topk(s, n, n, "none", "hann", 0, None, k, 18.0, 200.0)
+    P = oracle.batch_spectrum(s, n, n, "none", "hann")
+    lo, hi = int(np.ceil(n / 200.0)), min(int(np.floor(n / 18.0)), n // 2 - 1)
+    for w in range(P.shape[0]):
+        bins = np.arange(lo, hi + 1)
+        order = bins[np.lexsort((bins, -P[w, lo:hi + 1]))][:k]
+        assert np.array_equal(got[w, :, 0].astype(int), order)
+        assert np.array_equal(got[w, :, 1], P[w, order])
+
+
+@pytest.mark.parametrize("n", [32, 64, 512, 4096])
+def test_inverse_vs_numpy_irfft(n):
+    rng = np.random.default_rng(n)
+    packed = rng.standard_normal(n)
+    x = oracle.fft_real_inverse(packed)
+    X = np.zeros(n // 2 + 1, complex)
+    X[: n // 2] = packed[0::2] + 1j * packed[1::2]
+    X[0] = packed[0]  # in[1] ignored, Nyquist 0 (build-defined contract, wavespec_oracle.c)
+    assert np.max(np.abs(x - np.fft.irfft(X, n))) <= 1e-13 * max(1.0, np.max(np.abs(x))) * np.log2(n)
+
+
+@pytest.mark.parametrize("n", [32, 1024, 4096])
+def test_inverse_round_trip(n):
+    """inverse(forward(x)) == x for x without a Nyquist component."""
+    x = synth.random_walk(n, n + 5)
+    alt = (-1.0) ** np.arange(n)
+    x = x - alt * (x @ alt) / n
+    back = oracle.fft_real_inverse(oracle.window_spectrum(x, "none", "none", output="packed"))
+    assert np.max(np.abs(back - x)) <= 1e-13 * np.max(np.abs(x)) * np.log2(n)
+
+
+@pytest.mark.parametrize("n", [4, 64, 1024, 4096])
+def test_phase_unwrap_vs_numpy(n):
+    """CalculateFFTPhase/UnwrapPhase/CalculateGroupDelay == numpy angle/unwrap/gradient on the
+    reference's n = N arrays (upper half zero)."""
+    x = synth.random_walk(n, n + 1)
+    # detrend "none": a mean-removed window's X_0 is rounding noise with an arbitrary phase
+    packed = oracle.window_spectrum(x, "none", "hann", output="packed")
+    ph, u, gd = oracle.phase_unwrap(packed)
+    X = packed[0::2] + 1j * packed[1::2]
+    full = np.concatenate([np.angle(X), np.zeros(n - n // 2)])
+    uf = np.unwrap(full)
+    gf = np.clip(-np.gradient(uf), -100.0, 100.0)
+    assert np.max(np.abs(ph - full[: n // 2])) <= 1e-15  # libm atan2 vs numpy's: last-ulp
+    assert np.max(np.abs(u - uf[: n // 2])) <= 1e-10
+    assert np.max(np.abs(gd - gf[: n // 2])) <= 1e-10
+
+
+def test_batch_phase_and_topk_phase_consistent():
+    n, hop = 512, 100
+    s = synth.random_walk(20 * hop + n, 4)
+    ph = oracle.batch_phase(s, n, hop, "iir", "hann", 300)
+    tk = oracle.batch_topk_phase(s, n, hop, "iir", "hann", 300, None, 5, 9.0, 200.0)
+    tk4 = oracle.batch_topk(s, n, hop, "iir", "hann", 300, None, 5, 9.0, 200.0)
+    assert np.array_equal(tk[:, :, :4], tk4)
+    assert np.array_equal(ph[:, 0], oracle.batch_spectrum(s, n, hop, "iir", "hann", 300))
+    for w in range(ph.shape[0]):
+        packed = oracle.window_spectrum(s[w * hop: w * hop + n], "iir", "hann", 300, output="packed")
+        _, u, gd = oracle.phase_unwrap(packed)
+        assert np.array_equal(ph[w, 1], u) and np.array_equal(ph[w, 2], gd)
+        b = tk[w, :, 0].astype(int)
+        assert np.array_equal(tk[w, :, 4], u[b]) and np.array_equal(tk[w, :, 5], gd[b])
