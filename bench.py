@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="north_star", choices=["c2", "c3", "north_star", "c4", "c5"])
+    ap.add_argument("--config", default="north_star",
+                    choices=["c2", "c3", "north_star", "c4", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -109,6 +110,21 @@ def cpu_baseline(d_series, cfg: dict, budget_s: float) -> dict:
     lib = oracle.lib()
     lib.ora_set_threads(1)
     n, hop = cfg["n"], cfg["hop"]
+    out = cfg.get("output", "power")
+    args = (n, hop, cfg["detrend"], cfg["window"], cfg.get("trend_period", 0))
+
+    def work(seg):
+        if out == "inverse":
+            for row in seg.reshape(-1, n):
+                oracle.fft_real_inverse(row)
+        elif out == "phase":
+            oracle.batch_phase(seg, *args, kalman=oracle.KALMAN_DEFAULTS)
+        elif out in ("topk", "topk_phase"):
+            f = oracle.batch_topk if out == "topk" else oracle.batch_topk_phase
+            f(seg, *args, oracle.KALMAN_DEFAULTS, 8, 18.0, 200.0)
+        else:
+            oracle.batch_spectrum(seg, *args, kalman=oracle.KALMAN_DEFAULTS)
+
     chunk = 256
     done, spent = 0, 0.0
     max_w = cfg["windows"]
@@ -116,15 +132,14 @@ def cpu_baseline(d_series, cfg: dict, budget_s: float) -> dict:
         take = min(chunk, max_w - done)
         seg = d_series[done * hop: (done + take - 1) * hop + n].double().cpu().numpy()
         t0 = time.perf_counter()
-        oracle.batch_spectrum(seg, n, hop, cfg["detrend"], cfg["window"], cfg.get("trend_period", 0),
-                              kalman=oracle.KALMAN_DEFAULTS)
+        work(seg)
         spent += time.perf_counter() - t0
         done += take
     dt = spent
     return {"value": done / dt, "unit": "windows/s", "cores": 1, "kind": "port",
             "sample": f"first {done} windows of the same {cfg['windows']}x{n} workload (hop={hop}, "
-                      f"{cfg['detrend']} detrend, {cfg['window']} window), oracle/wavespec_oracle.c -O3, "
-                      f"1 thread, {dt:.1f} s"}
+                      f"{cfg['detrend']} detrend, {cfg['window']} window, output {out}), "
+                      f"oracle/wavespec_oracle.c -O3, 1 thread, {dt:.1f} s"}
 
 
 def load_traffic(config: str):
@@ -221,11 +236,19 @@ def main():
     f32 = cfg["precision"] == "f32"
     tdt = torch.float32 if f32 else torch.float64
     length = (w - 1) * hop + n
-    d_series = synth.random_walk_torch(length, cfg["seed"] + 1000 * rank, dev, tdt)  # resident in HBM
-    rec = n // 2
-    d_out = torch.empty(w * rec, dtype=tdt, device=dev)
-    plan = bridge.Plan(local_rank, n, hop, w, cfg["detrend"], cfg["window"], cfg["trend_period"],
-                       cfg["precision"], "power")
+    output = cfg.get("output", "power")
+    if output == "inverse":  # rows of packed spectra (random, resident in HBM)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(cfg["seed"] + 1000 * rank)
+        d_series = torch.randn(w * n, dtype=tdt, device=dev, generator=gen)
+        plan = bridge.Plan.inverse(local_rank, n, w)
+    else:
+        d_series = synth.random_walk_torch(length, cfg["seed"] + 1000 * rank, dev, tdt)  # resident in HBM
+        plan = bridge.Plan(local_rank, n, hop, w, cfg["detrend"], cfg["window"], cfg["trend_period"],
+                           cfg["precision"], output)
+        if output in ("topk", "topk_phase"):
+            plan.set_topk(8, 18.0, 200.0)  # the reference's scan (1.1.0:22-23)
+    d_out = torch.empty(w * plan.record, dtype=tdt, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -269,7 +292,11 @@ def main():
             "dtype": "f32" if f32 else "f64",
             "data": "synthetic (random-walk close prices generated on device, seed per rank)",
             "config": {"workload": f"{args.config}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, "
-                                   f"{cfg['detrend']} detrend, {cfg['window']} window, |X|^2 k<N/2",
+                                   f"{cfg['detrend']} detrend, {cfg['window']} window, " + {
+                                       "power": "|X|^2 k<N/2", "topk": "top-8 bins in periods [18, 200]",
+                                       "phase": "[|X|^2, unwrapped phase, group delay] k<N/2",
+                                       "topk_phase": "top-8 bins + phase/delay in periods [18, 200]",
+                                       "inverse": "inverse real FFT of packed spectra"}[output],
                        "windows_per_gpu": w, "window_len": n, "hop": hop, "parallelism": f"windows sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -31,6 +31,8 @@
 //  * Detrend arithmetic is fp64 in both precisions (prices ~1.1 minus a trend
 //    of the same size: fp32 would cancel catastrophically).
 #pragma once
+#include <type_traits>
+
 #include "wsp_internal.h"
 
 namespace wsp {
@@ -118,7 +120,9 @@ template <int LOG2N> struct Geo {
     static constexpr int M = N / 2;           // complex points
     static constexpr int LOG2M = LOG2N - 1;
     static constexpr int TPW = M / 16;        // threads per window
-    static constexpr int WPB = kBlock / TPW;  // windows per workgroup
+    static constexpr int BLOCK = TPW > kBlock ? TPW : kBlock;  // threads per workgroup
+    static constexpr int WPB = BLOCK / TPW;                    // windows per workgroup
+    static constexpr int NWV = TPW >= 64 ? TPW / 64 : 1;       // waves per window
     static constexpr int SLOT = M + M / 16;   // padded complex slots per window
     static constexpr int Q = LOG2M - 3;
     static constexpr int N16 = Q / 4, REM = Q % 4;
@@ -132,7 +136,7 @@ template <int LOG2N> struct Geo {
     }
     static constexpr int R0 = radix(0);
     static constexpr int BPT0 = 16 / R0;
-    static_assert(TPW >= 1 && TPW <= kBlock, "window size out of range");
+    static_assert(TPW >= 1 && TPW <= 512, "window size out of range");
 };
 
 __device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
@@ -267,6 +271,160 @@ __device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cp
     }
 }
 
+// Lane exchanges that stay in the VALU: DPP row/quad permutations and the gfx950
+// v_permlane16/32_swap (no LDS-crossbar round trip as with ds_bpermute).
+template <int CTRL> __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <typename T> struct Bits;
+template <> struct Bits<double> {
+    static constexpr int W = 2;
+    __device__ static void split(double v, unsigned (&u)[2]) {
+        const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+        u[0] = (unsigned)x;
+        u[1] = (unsigned)(x >> 32);
+    }
+    __device__ static double join(const unsigned (&u)[2]) {
+        return __builtin_bit_cast(double, (unsigned long long)u[0] | ((unsigned long long)u[1] << 32));
+    }
+};
+template <> struct Bits<float> {
+    static constexpr int W = 1;
+    __device__ static void split(float v, unsigned (&u)[1]) { u[0] = __builtin_bit_cast(unsigned, v); }
+    __device__ static float join(const unsigned (&u)[1]) { return __builtin_bit_cast(float, u[0]); }
+};
+
+// Argmax of (p, b) under (p desc, b asc) over aligned segments of SW lanes (SW = 1..64, a power
+// of two); every lane of a segment ends with the segment's winner.  The combine is idempotent,
+// so the mirror steps and both halves of a permlane swap can be folded in unconditionally.
+template <int SW, typename T> __device__ __forceinline__ void seg_argmax(T &p, int &b) {
+    using BT = Bits<T>;
+    auto comb = [&](T op, int ob) {
+        if (op > p || (op == p && ob < b)) {
+            p = op;
+            b = ob;
+        }
+    };
+    auto dpp_step = [&](auto ctrl) {
+        constexpr int C = decltype(ctrl)::value;
+        unsigned u[BT::W];
+        BT::split(p, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) u[i] = dpp_u32<C>(u[i]);
+        comb(BT::join(u), (int)dpp_u32<C>((unsigned)b));
+    };
+    auto swap_step = [&](auto which) {
+        unsigned u[BT::W], r0[BT::W], r1[BT::W];
+        BT::split(p, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) {
+            const auto r = decltype(which)::value == 16 ? __builtin_amdgcn_permlane16_swap(u[i], u[i], false, false)
+                                                         : __builtin_amdgcn_permlane32_swap(u[i], u[i], false, false);
+            r0[i] = r[0];
+            r1[i] = r[1];
+        }
+        const auto rb = decltype(which)::value == 16
+                            ? __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false)
+                            : __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+        comb(BT::join(r0), (int)rb[0]);
+        comb(BT::join(r1), (int)rb[1]);
+    };
+    if constexpr (SW >= 2) dpp_step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+    if constexpr (SW >= 4) dpp_step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+    if constexpr (SW >= 8) dpp_step(std::integral_constant<int, 0x141>{});  // row_half_mirror
+    if constexpr (SW >= 16) dpp_step(std::integral_constant<int, 0x140>{}); // row_mirror
+    if constexpr (SW >= 32) swap_step(std::integral_constant<int, 16>{});   // rows 2i <-> 2i+1
+    if constexpr (SW >= 64) swap_step(std::integral_constant<int, 32>{});   // lanes 0-31 <-> 32-63
+}
+
+// Same argmax as seg_argmax in two cheaper reductions: max of p (DPP-moved halves + v_max),
+// then the minimum bin among the lanes whose own p equals that max.  Identical result for
+// non-NaN p.
+template <int SW, typename T> __device__ __forceinline__ void seg_argmax2(T p0, int b0, T &wp, int &wb) {
+    using BT = Bits<T>;
+    T m = p0;
+    auto dpp_max = [&](auto ctrl) {
+        constexpr int C = decltype(ctrl)::value;
+        unsigned u[BT::W];
+        BT::split(m, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) u[i] = dpp_u32<C>(u[i]);
+        m = fmax(m, BT::join(u));
+    };
+    auto swap_max = [&](auto which) {
+        unsigned u[BT::W], r0[BT::W], r1[BT::W];
+        BT::split(m, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) {
+            const auto r = decltype(which)::value == 16 ? __builtin_amdgcn_permlane16_swap(u[i], u[i], false, false)
+                                                         : __builtin_amdgcn_permlane32_swap(u[i], u[i], false, false);
+            r0[i] = r[0];
+            r1[i] = r[1];
+        }
+        m = fmax(m, fmax(BT::join(r0), BT::join(r1)));
+    };
+    int b = p0 == m ? b0 : 0x7fffffff;  // placeholder: recomputed after the max is final
+    if constexpr (SW >= 2) dpp_max(std::integral_constant<int, 0xB1>{});
+    if constexpr (SW >= 4) dpp_max(std::integral_constant<int, 0x4E>{});
+    if constexpr (SW >= 8) dpp_max(std::integral_constant<int, 0x141>{});
+    if constexpr (SW >= 16) dpp_max(std::integral_constant<int, 0x140>{});
+    if constexpr (SW >= 32) swap_max(std::integral_constant<int, 16>{});
+    if constexpr (SW >= 64) swap_max(std::integral_constant<int, 32>{});
+    b = p0 == m ? b0 : 0x7fffffff;
+    auto dpp_min = [&](auto ctrl) { b = min(b, (int)dpp_u32<decltype(ctrl)::value>((unsigned)b)); };
+    auto swap_min = [&](auto which) {
+        const auto r = decltype(which)::value == 16 ? __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false)
+                                                     : __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+        b = min(b, min((int)r[0], (int)r[1]));
+    };
+    if constexpr (SW >= 2) dpp_min(std::integral_constant<int, 0xB1>{});
+    if constexpr (SW >= 4) dpp_min(std::integral_constant<int, 0x4E>{});
+    if constexpr (SW >= 8) dpp_min(std::integral_constant<int, 0x141>{});
+    if constexpr (SW >= 16) dpp_min(std::integral_constant<int, 0x140>{});
+    if constexpr (SW >= 32) swap_min(std::integral_constant<int, 16>{});
+    if constexpr (SW >= 64) swap_min(std::integral_constant<int, 32>{});
+    wp = m;
+    wb = b;
+}
+
+// k rounds of the top-k scan for one lane holding NB bins kmin + t + TPW i (i < NB).  Round r's
+// winner (power desc, bin asc) goes to on_win(r, wp, wb, own); the owner retires its bin.
+template <int NB, int SW, int TPW, typename T, typename XF, typename WF>
+__device__ __forceinline__ void topk_rounds(int t, int kmin, int span, int k, XF power_of, WF on_win) {
+    constexpr int kNone = 0x7fffffff;
+    T p[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) p[i] = t + TPW * i < span ? power_of(kmin + t + TPW * i) : T(-1);
+    T bp;
+    int bi;
+    auto lane_best = [&]() {  // ascending i = ascending bin: strict '>' keeps the lower bin
+        bp = T(-1);
+        bi = -1;
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+            if (p[i] > bp) {
+                bp = p[i];
+                bi = i;
+            }
+    };
+    lane_best();
+    for (int r = 0; r < k; ++r) {
+        const int mb = bi >= 0 ? kmin + t + TPW * bi : kNone;
+        T wp;
+        int wb;
+        seg_argmax2<SW>(bp, mb, wp, wb);
+        if (wp < T(0)) wb = kNone;  // nothing left in range
+        const bool own = wb != kNone && wb == mb;
+        if (own) {
+#pragma unroll
+            for (int i = 0; i < NB; ++i)
+                if (i == bi) p[i] = T(-1);
+            lane_best();
+        }
+        on_win(r, wp, wb, own);
+    }
+}
+
 // Phase, unwrap and group delay of one window (CalculateFFTPhase, UnwrapPhase,
 // CalculateGroupDelay: L/WaveSpecZZ_1.0.4-new.mq5:1040-1120, called at :3225-3227
 // with n = N over the GPU unpack of :3183-3196, i.e. X_k for k < N/2 and zeros
@@ -313,11 +471,11 @@ __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, doub
         if (lt >= d) incl += up;
     }
     int K = incl - sum;  // corrections of every bin < k0
-    if constexpr (TPW == 128) {
-        int *sb = reinterpret_cast<int *>(scanbuf + 4);
-        if (t == 63) sb[0] = incl;
+    if constexpr (TPW >= 128) {  // add the totals of the window's earlier waves
+        int *sb = reinterpret_cast<int *>(scanbuf + 8);
+        if (lt == 63) sb[t >> 6] = incl;
         __syncthreads();
-        if (t >= 64) K += sb[0];
+        for (int i = 0; i < (t >> 6); ++i) K += sb[i];
     }
     const double um1 = fma((double)K, k2Pi, ph[0]);  // u[k0 - 1]
 #pragma unroll
@@ -368,18 +526,23 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
-__global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
+__global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
     using G = Geo<LOG2N>;
     using v2 = typename V2<T>::t;
-    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B;
+    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B, NWV = G::NWV;
     constexpr int R0 = G::R0, BPT0 = G::BPT0;
     constexpr bool kPrefetch = !(VAR & kVarNoPrefetch);
     constexpr bool kSplit = VAR & kVarSplitLds;
     constexpr int kCplx = WPB * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));
     constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
     constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
-    constexpr int kScan = 16 * 8;
     constexpr bool kPhase = OUT == kOutPhase || OUT == kOutTopKPhase;
+    // scan scratch: 16 doubles, + (top-k, two waves per window) two sorted lists and the merge
+    // scan scratch: doubles [0, 8) wave totals of the mean / IIR reductions, [8, 16) the unwrap's
+    // int wave totals; + (top-k with several waves per window) one sorted list per wave;
+    // + (kOutTopKPhase) the winners of every window
+    constexpr int kScan = 16 * 8 + ((OUT == kOutTopK || OUT == kOutTopKPhase) && TPW >= 128 ? NWV * 64 * (8 + 4) : 0) +
+                          (OUT == kOutTopKPhase ? WPB * (M < 64 ? M : 64) * 4 : 0);
     static_assert(!kPhase || sizeof(T) == 8, "phase outputs are fp64");
     __shared__ __attribute__((aligned(16))) char smem[kMain + kScan];
     double *scanbuf = reinterpret_cast<double *>(smem + kMain);
@@ -429,11 +592,13 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
             constexpr int SW = TPW < 64 ? TPW : 64;
 #pragma unroll
             for (int off = SW / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, SW);
-            if constexpr (TPW == 128) {
+            if constexpr (TPW >= 128) {  // one window per workgroup: combine its waves
                 __syncthreads();  // scanbuf reuse across groups
                 if ((tid & 63) == 0) scanbuf[tid >> 6] = s;
                 __syncthreads();
-                s = scanbuf[0] + scanbuf[1];
+                s = 0.0;
+#pragma unroll
+                for (int i = 0; i < NWV; ++i) s += scanbuf[i];
             }
             const double mean = s / (double)N;
 #pragma unroll
@@ -473,19 +638,23 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
                 if (lt >= d) v = a.apow[j] * up + v;
             }
             double carry = __shfl_up(v, 1, SW);
-            if constexpr (TPW == 128) {
-                if (t == 63) scanbuf[0] = v;
+            if constexpr (TPW >= 128) {
+                // state entering wave wv: G = sum_(i<wv) A^(wv-1-i) T_i over the earlier waves'
+                // local totals T_i, A = alpha^(32*64) (one wave's 64 chunks)
+                if (lt == 63) scanbuf[t >> 6] = v;
                 __syncthreads();
-                if (t >= 64) {
-                    const double v0 = scanbuf[0];
+                const int wv = t >> 6;
+                if (wv > 0) {
+                    double G = 0.0;
+                    for (int i = 0; i < wv; ++i) G = a.apow[6] * G + scanbuf[i];
                     double p = 1.0;
                     const int m = lt + 1;
 #pragma unroll
                     for (int j = 0; j < 7; ++j)
                         if ((m >> j) & 1) p *= a.apow[j];
-                    v = p * v0 + v;
+                    v = p * G + v;
                     carry = __shfl_up(v, 1, SW);
-                    if (lt == 0) carry = v0;
+                    if (lt == 0) carry = G;
                 }
             }
             if (t == 0) carry = 0.0;
@@ -656,99 +825,148 @@ __global__ __launch_bounds__(kBlock, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 
         // unwrapped phase / group delay of bins [16t, 16t + 16) (kept in registers
         // through the top-k scan for kOutTopKPhase)
         double pw[kPhase ? 16 : 1], u[kPhase ? 16 : 1], gd[kPhase ? 16 : 1];
-        if constexpr (kPhase) {
+        if constexpr (OUT == kOutPhase) {
             const cpx<double> *xrow = reinterpret_cast<const cpx<double> *>(lbase);
             __syncthreads();  // X row complete
             phase_chunk<LOG2N>(xrow, t, scanbuf, pw, u, gd);
-            if constexpr (OUT == kOutPhase) {
-                // record [P | unwrapped phase | group delay]: 16 contiguous bins per lane
-                if (active) {
-                    T *rec = a.out + w * (int64_t)(3 * M) + 16 * t;
+            {
+                // record [P | unwrapped phase | group delay]: each row staged through this window's
+                // LDS slot (2 pad doubles per 16 keep pairs 16-B aligned and the lane-strided writes
+                // conflict-free), then written with contiguous 16-B NT stores like the power row
+                double *srow = reinterpret_cast<double *>(lbase);
+                auto pidx = [](int k) { return k + 2 * (k >> 4); };
+                auto put = [&](const double(&val)[16], int row) {
+                    __syncthreads();  // previous reads of the slot are done
 #pragma unroll
-                    for (int j = 0; j < 16; j += 2) {
-                        __builtin_nontemporal_store(v2{pw[j], pw[j + 1]}, reinterpret_cast<v2 *>(rec + j));
-                        __builtin_nontemporal_store(v2{u[j], u[j + 1]}, reinterpret_cast<v2 *>(rec + M + j));
-                        __builtin_nontemporal_store(v2{gd[j], gd[j + 1]}, reinterpret_cast<v2 *>(rec + 2 * M + j));
+                    for (int j = 0; j < 16; j += 2)
+                        *reinterpret_cast<v2 *>(srow + pidx(16 * t + j)) = v2{val[j], val[j + 1]};
+                    __syncthreads();
+                    if (active) {
+                        T *dst = a.out + w * (int64_t)(3 * M) + row * M;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int k = 2 * (t + TPW * j);
+                            __builtin_nontemporal_store(*reinterpret_cast<const v2 *>(srow + pidx(k)),
+                                                        reinterpret_cast<v2 *>(dst + k));
+                        }
                     }
-                }
+                };
+                put(pw, 0);
+                put(u, 1);
+                put(gd, 2);
             }
         }
         if constexpr (OUT == kOutTopK || OUT == kOutTopKPhase) {
-            // Top-k bin scan (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554):
-            // k rounds of argmax over bins [kmin, kmax] ordered (power desc, bin asc) -- the
-            // order the reference's strict-'>' insertion in ascending bin order produces.  The
-            // winner's owner writes [bin, power, Re X, Im X] and retires the bin (NaN power).
-            cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
+            // Top-k bin scan (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554) in the
+            // order (power desc, bin asc) that the reference's strict-'>' insertion in ascending bin
+            // order produces.  Each lane keeps the powers of its bins kmin + t + TPW i in registers;
+            // k rounds of a wave-wide argmax (xor shuffles, no barrier) pick the winners and the
+            // owner retires its bin.  With two waves per window (N = 4096) each wave builds its own
+            // sorted list and the two lists merge by rank counting behind one barrier.  The X row
+            // is left intact: kOutTopKPhase computes the phases after the scan and the owners of
+            // the winners' chunks add them to the records.
+            const cpx<T> *xrow = reinterpret_cast<const cpx<T> *>(lbase);
             constexpr int SW = TPW < 64 ? TPW : 64;
             constexpr int kNone = 0x7fffffff;
             constexpr int RW = OUT == kOutTopKPhase ? 6 : 4;  // record width
             auto xi = [](int k) { return kPhase ? pad16(k) : k; };
             __syncthreads();  // X row complete
-            for (int s = 0; s < a.topk; ++s) {
-                T bp = T(-1);
-                int bb = kNone;
-                for (int b = a.kmin + t; b <= a.kmax; b += TPW) {
-                    const cpx<T> x = xrow[xi(b)];
-                    const T p = x.re * x.re + x.im * x.im;
-                    if (p > bp || (p == bp && b < bb)) {
-                        bp = p;
-                        bb = b;
-                    }
-                }
+            const int span = a.kmax - a.kmin + 1;
+            T *recw = a.out + w * (int64_t)(RW * a.topk);
+            auto write_x = [&](T *rec, int b, T pw_) {
+                const cpx<T> x = xrow[xi(b)];
+                rec[0] = T(b);
+                rec[1] = pw_;
+                rec[2] = x.re;
+                rec[3] = x.im;
+            };
+            auto write_empty = [&](T *rec) {
+                rec[0] = T(-1);
+                rec[1] = T(-1);
 #pragma unroll
-                for (int off = SW / 2; off >= 1; off >>= 1) {
-                    const T op = __shfl_xor(bp, off, SW);
-                    const int ob = __shfl_xor(bb, off, SW);
-                    if (op > bp || (op == bp && ob < bb)) {
-                        bp = op;
-                        bb = ob;
+                for (int j = 2; j < RW; ++j) rec[j] = T(0);
+            };
+            constexpr int KW = M < 64 ? M : 64;  // winners that can exist per window (k <= 64, span <= M)
+            constexpr int LST = TPW >= 128 ? NWV * 64 : 0;  // list entries (several waves per window)
+            int *win = reinterpret_cast<int *>(scanbuf + 16 + LST) + LST + slot * KW;  // kOutTopKPhase winners
+            const int lt = t & (SW - 1);
+            T cp = T(-1);  // TPW >= 128: this lane's entry of its wave's sorted list
+            int cb = kNone;
+            auto power_of = [&](int b) {
+                const cpx<T> x = xrow[xi(b)];
+                return x.re * x.re + x.im * x.im;
+            };
+            auto on_win = [&](int r, T wp, int wb, bool own) {
+                if constexpr (TPW >= 128) {
+                    if (lt == r) {
+                        cp = wp;
+                        cb = wb;
+                    }
+                } else {  // one wave segment per window: round r's winner is slot r
+                    T *rec = recw + RW * r;
+                    if (own && active) write_x(rec, wb, wp);
+                    if (wb == kNone && t == 0 && active) write_empty(rec);
+                    if constexpr (RW == 6) {
+                        if (t == 0 && r < KW) win[r] = wb;
                     }
                 }
-                if constexpr (TPW == 128) {
-                    int *sb = reinterpret_cast<int *>(scanbuf + 2);
-                    if ((tid & 63) == 0) {
-                        scanbuf[tid >> 6] = (double)bp;
-                        sb[tid >> 6] = bb;
-                    }
-                    __syncthreads();
-                    const T p0 = (T)scanbuf[0], p1 = (T)scanbuf[1];
-                    const int b0 = sb[0], b1 = sb[1];
-                    const bool second = p1 > p0 || (p1 == p0 && b1 < b0);
-                    bp = second ? p1 : p0;
-                    bb = second ? b1 : b0;
+            };
+            // bins per lane: uniform branch to a register array of just that size
+            const int nbl = span <= 0 ? 1 : (span + TPW - 1) / TPW;
+            if (nbl <= 1) topk_rounds<1, SW, TPW, T>(t, a.kmin, span, a.topk, power_of, on_win);
+            else if (nbl <= 2) topk_rounds<2, SW, TPW, T>(t, a.kmin, span, a.topk, power_of, on_win);
+            else if (nbl <= 4) topk_rounds<4, SW, TPW, T>(t, a.kmin, span, a.topk, power_of, on_win);
+            else if (nbl <= 8) topk_rounds<8, SW, TPW, T>(t, a.kmin, span, a.topk, power_of, on_win);
+            else topk_rounds<16, SW, TPW, T>(t, a.kmin, span, a.topk, power_of, on_win);
+            if constexpr (TPW >= 128) {
+                double *lp = scanbuf + 16;                              // [NWV][64] powers
+                int *lb = reinterpret_cast<int *>(scanbuf + 16 + LST);  // [NWV][64] bins
+                const int wv = t >> 6;
+                if (lt < a.topk) {
+                    lp[64 * wv + lt] = (double)cp;
+                    lb[64 * wv + lt] = cb;
                 }
-                T *rec = a.out + w * (int64_t)(RW * a.topk) + RW * s;
-                if (bb != kNone) {
-                    if ((bb - a.kmin) % TPW == t) {
-                        const cpx<T> x = xrow[xi(bb)];
-                        if (active) {
-                            rec[0] = T(bb);
-                            rec[1] = bp;
-                            rec[2] = x.re;
-                            rec[3] = x.im;
-                        }
-                        xrow[xi(bb)] = {T(__builtin_nan("")), T(__builtin_nan(""))};
+                __syncthreads();
+                int rank = lt, nother = 0;  // rank among all lists (bins are distinct across lists)
+                for (int v2 = 0; v2 < NWV; ++v2) {
+                    if (v2 == wv) continue;
+                    for (int j = 0; j < a.topk; ++j) {
+                        const T op = (T)lp[64 * v2 + j];
+                        const int ob = lb[64 * v2 + j];
+                        nother += ob != kNone;
+                        rank += ob != kNone && (op > cp || (op == cp && ob < cb));
                     }
-                    if constexpr (RW == 6) {  // phase fields from the owner of bin bb's chunk
-                        if ((bb >> 4) == t && active) {
-                            double ub = 0.0, gb = 0.0;
+                }
+                const int nvalid = (int)__popcll(__ballot(lt < a.topk && cb != kNone)) + nother;
+                const bool mine = lt < a.topk && cb != kNone && rank < a.topk;
+                if (mine && active) write_x(recw + RW * rank, cb, cp);
+                if (wv == 0 && lt >= nvalid && lt < a.topk && active) write_empty(recw + RW * lt);
+                if constexpr (RW == 6) {
+                    if (mine) win[rank] = cb;
+                    if (wv == 0 && lt >= nvalid && lt < a.topk) win[lt] = kNone;
+                }
+            }
+            if constexpr (RW == 6) {
+                // phases of the (unmodified) X row, then the owner of each winner's chunk adds
+                // [unwrapped phase, group delay] to that slot
+                __syncthreads();  // winners list complete
+                phase_chunk<LOG2N>(reinterpret_cast<const cpx<double> *>(lbase), t, scanbuf, pw, u, gd);
+                const int nk = a.topk < KW ? a.topk : KW;
+                for (int s2 = 0; s2 < nk; ++s2) {
+                    const int b = win[s2];
+                    if (b != kNone && (b >> 4) == t && active) {
+                        double ub = 0.0, gb = 0.0;
 #pragma unroll
-                            for (int j = 0; j < 16; ++j)
-                                if ((bb & 15) == j) {
-                                    ub = u[j];
-                                    gb = gd[j];
-                                }
-                            rec[4] = ub;
-                            rec[5] = gb;
-                        }
+                        for (int j = 0; j < 16; ++j)
+                            if ((b & 15) == j) {
+                                ub = u[j];
+                                gb = gd[j];
+                            }
+                        T *rec = recw + RW * s2;
+                        rec[4] = ub;
+                        rec[5] = gb;
                     }
-                } else if (t == 0 && active) {  // fewer than k bins in range: (-1, -1) slots
-                    rec[0] = T(-1);
-                    rec[1] = T(-1);
-#pragma unroll
-                    for (int j = 2; j < RW; ++j) rec[j] = T(0);
                 }
-                if constexpr (TPW == 128) __syncthreads();  // retirement visible to both waves
             }
         }
         if constexpr (OUT == kOutPower) {

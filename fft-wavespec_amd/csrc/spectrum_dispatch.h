@@ -66,21 +66,23 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
 // AoS exchange at 2 waves/SIMD.
 constexpr int kDefaultVar = kVarNoPrefetch | kVarNtStore | kVarSplitLds;
 constexpr int kDefaultGrid = 32768;
-template <typename T, int DETREND, int OUT> constexpr int default_var() {
-    // the f32 mean path converts every sample to fp64 for the reduction and spills at 168
-    return (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean))
+template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var() {
+    // the f32 mean path converts every sample to fp64 for the reduction and spills at 168;
+    // N > 4096 runs one 256/512-thread workgroup per window, where the split exchange cannot
+    // raise occupancy (LDS and VGPRs allow 2 waves/SIMD either way)
+    return (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
                ? (kVarNoPrefetch | kVarNtStore)
                : kDefaultVar;
 }
 
-template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, DETREND, OUT>()>
+template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
 hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
     using G = Geo<LOG2N>;
     const SpecArgs<T> a = make_args<T>(L, G::WPB);
     int64_t grid = L.grid > 0 ? L.grid : kDefaultGrid;
     if (grid > a.n_groups) grid = a.n_groups;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((spectrum_kernel<T, LOG2N, DETREND, OUT, WCLASS, VAR>), dim3((unsigned)grid), dim3(kBlock),
+    hipLaunchKernelGGL((spectrum_kernel<T, LOG2N, DETREND, OUT, WCLASS, VAR>), dim3((unsigned)grid), dim3(G::BLOCK),
                        0, stream, a);
     return hipGetLastError();
 }
@@ -138,6 +140,8 @@ template <typename T, int OSET = kSetBase> hipError_t dispatch_n(const SpectrumL
     case 10: return dispatch_detrend<T, 10, OSET>(L, s);
     case 11: return dispatch_detrend<T, 11, OSET>(L, s);
     case 12: return dispatch_detrend<T, 12, OSET>(L, s);
+    case 13: return dispatch_detrend<T, 13, OSET>(L, s);
+    case 14: return dispatch_detrend<T, 14, OSET>(L, s);
     default: return hipErrorInvalidValue;
     }
 }

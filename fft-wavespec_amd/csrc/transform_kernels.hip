@@ -22,7 +22,7 @@ namespace wsp {
 namespace core {
 
 template <int LOG2N>
-__global__ __launch_bounds__(kBlock, 2) void inverse_kernel(const double *__restrict__ in, double *__restrict__ out,
+__global__ __launch_bounds__(Geo<LOG2N>::BLOCK, 2) void inverse_kernel(const double *__restrict__ in, double *__restrict__ out,
                                                            const cpx<double> *__restrict__ tw, int64_t n_windows,
                                                            int64_t n_groups) {
     using G = Geo<LOG2N>;
@@ -46,7 +46,9 @@ __global__ __launch_bounds__(kBlock, 2) void inverse_kernel(const double *__rest
         // stored conjugated in natural order; thread 0 also forms Z_(M/2) = conj X_(M/2).
         __syncthreads();  // the previous group's final-pass reads of this slot are done
         const int pa0 = pad16(t), pb0 = pad16(M - t);
-#pragma unroll
+        // unroll 2: fully unrolled, the scheduler hoists all 16 sample loads and spills (up to
+        // 324 B/lane at N = 16384); pairs of iterations keep it at zero scratch for every N
+#pragma unroll 2
         for (int j = 0; j < 8; ++j) {
             const int k = t + TPW * j;
             // pad16(t + TPW j), pad16(M - t - TPW j) with the j part folded into the ds offset
@@ -188,7 +190,7 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
         const int64_t groups = (L.n_windows + Geo<LG>::WPB - 1) / Geo<LG>::WPB;                               \
         int64_t grid = L.grid > 0 ? L.grid : 32768;                                                           \
         if (grid > groups) grid = groups;                                                                     \
-        hipLaunchKernelGGL(inverse_kernel<LG>, dim3((unsigned)grid), dim3(kBlock), 0, stream, L.in, L.out, tw, \
+        hipLaunchKernelGGL(inverse_kernel<LG>, dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, L.out, tw, \
                            L.n_windows, groups);                                                              \
         return hipGetLastError();                                                                             \
     }
@@ -201,6 +203,8 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
         INV_CASE(10)
         INV_CASE(11)
         INV_CASE(12)
+        INV_CASE(13)
+        INV_CASE(14)
     default: return hipErrorInvalidValue;
     }
 #undef INV_CASE

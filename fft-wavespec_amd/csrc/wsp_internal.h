@@ -7,11 +7,12 @@
 namespace wsp {
 
 // Smallest / largest window the single-workgroup kernel handles.  N = 2M,
-// M complex points per window live in one workgroup's LDS (SURVEY.md sec. 5
-// "Long-context analogue": N <= 4096 fp64 fits one workgroup).
+// M complex points per window live in one workgroup's registers (16 per
+// thread, M/16 threads) and LDS (AoS 16 B per point + pad: 136 KiB at
+// N = 16384, within gfx950's 160 KiB per workgroup).
 constexpr int kMinLog2N = 5;   // N = 32
-constexpr int kMaxLog2N = 12;  // N = 4096
-constexpr int kBlock = 128;    // threads per workgroup (2 waves)
+constexpr int kMaxLog2N = 14;  // N = 16384
+constexpr int kBlock = 128;    // minimum threads per workgroup (2 waves); M/16 when larger
 
 enum Detrend : int { kDetrendNone = 0, kDetrendMean = 1, kDetrendIir = 2, kDetrendKalman = 3 };
 enum Output : int { kOutPower = 0, kOutPacked = 1, kOutTopK = 2, kOutPhase = 3, kOutTopKPhase = 4 };

@@ -145,6 +145,67 @@ int kalman_main(int reps) {
     return 0;
 }
 
+template <int OUT, int VAR>
+float time_out(const SpectrumLaunch &L, hipStream_t s, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 2; ++i) CK((launch_one<double, 12, kDetrendNone, OUT, kWinCos, VAR>(L, s)));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i) CK((launch_one<double, 12, kDetrendNone, OUT, kWinCos, VAR>(L, s)));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1000.f / reps;
+}
+
+// Output-mode ablation at the north-star shape: where the top-k / phase time goes.
+int out_main(int reps) {
+    const int64_t W = 65536;
+    const int n = 4096;
+    double *x, *out, *tw;
+    CK(hipMalloc(&x, W * n * 8));
+    CK(hipMalloc(&out, W * n * 3 / 2 * 8));
+    CK(hipMalloc(&tw, n * 16));
+    std::vector<double> h(2 * n);
+    for (int k = 0; k < n; ++k) {
+        long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+        h[2 * k] = (double)cosl(a);
+        h[2 * k + 1] = (double)sinl(a);
+    }
+    CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_walk, dim3(4096), dim3(256), 0, 0, x, W * n);
+    CK(hipDeviceSynchronize());
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    SpectrumLaunch L{};
+    L.series = x; L.out = out; L.twiddle = tw; L.window = 1; L.hop = n; L.n_windows = W; L.log2n = 12;
+    L.kmin = 21; L.kmax = 227;  // periods [18, 200]
+    constexpr int AOS = kVarNoPrefetch | kVarNtStore;
+    for (int round = 0; round < 2; ++round) {
+        L.topk = 8;
+        const float pa = time_out<kOutPower, AOS>(L, s, reps);
+        const float ps = time_out<kOutPower, AOS | kVarSplitLds>(L, s, reps);
+        const float pk = time_out<kOutPacked, AOS>(L, s, reps);
+        L.topk = 0;
+        const float t0 = time_out<kOutTopK, AOS>(L, s, reps);
+        L.topk = 1;
+        const float t1 = time_out<kOutTopK, AOS>(L, s, reps);
+        L.topk = 8;
+        const float t8 = time_out<kOutTopK, AOS>(L, s, reps);
+        L.kmax = 22;
+        const float t8n = time_out<kOutTopK, AOS>(L, s, reps);
+        L.kmax = 227;
+        const float ph = time_out<kOutPhase, AOS>(L, s, reps);
+        const float tp = time_out<kOutTopKPhase, AOS>(L, s, reps);
+        printf("round %d  power-aos %.1f  power-split %.1f  packed %.1f | topk k=0 %.1f  k=1 %.1f  k=8 %.1f  "
+               "k=8/2 bins %.1f | phase %.1f  topk-phase %.1f us\n", round, pa, ps, pk, t0, t1, t8, t8n, ph, tp);
+        fflush(stdout);
+    }
+    return 0;
+}
+
 template <int VAR>
 float time_c4(const SpectrumLaunch &L, int reps) {
     hipEvent_t e0, e1;
@@ -196,6 +257,7 @@ int c4_main(int reps) {
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "kalman") return kalman_main(argc > 2 ? atoi(argv[2]) : 5);
     if (argc > 1 && std::string(argv[1]) == "c4") return c4_main(argc > 2 ? atoi(argv[2]) : 5);
+    if (argc > 1 && std::string(argv[1]) == "out") return out_main(argc > 2 ? atoi(argv[2]) : 20);
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;

@@ -42,6 +42,16 @@ CONFIGS = {
     "c3": dict(windows=65536, n=4096, hop=4096, precision="f32", detrend="kalman", window="hann", seed=11),
     "north_star": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann", seed=11),
     "c4": dict(windows=1048576, n=2048, hop=1, precision="f64", detrend="none", window="hann", seed=13),
+    # SURVEY 8f rows on the north-star shape (not the headline metric): fused consumers of the
+    # spectrum and the inverse transform
+    "ns_topk": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann", seed=11,
+                    output="topk"),
+    "ns_phase": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann", seed=11,
+                     output="phase"),
+    "ns_topk_phase": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann",
+                          seed=11, output="topk_phase"),
+    "inverse": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="none", seed=11,
+                    output="inverse"),
 }
 
 

@@ -89,7 +89,7 @@ MTB_API void gpu_shutdown(void);
 /* imports.mqh:7; caller FftProcessor::Run 1.1.0:518-531.  Real forward DFT
  * (unnormalised, e^{-2 pi i k n/N}) of in[0..len) into out[0..len):
  * out[2k] = Re X_k, out[2k+1] = Im X_k for k < len/2.  len: power of two,
- * 16..4096.  Synchronous. */
+ * 32..16384.  Synchronous. */
 MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out);
 
 /* imports.mqh:8-19: MUSIC/ESPRIT cycle extraction lives outside the
@@ -139,7 +139,7 @@ MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len,
  * 0 < k < len/2, X_0 = in[0] (in[1], Im X_0 of a real signal, is ignored),
  * X_{len/2} = 0 (no slot in the layout), out[n] = (1/len) sum_k X_k
  * e^{+2 pi i k n/len}.  inverse(forward(x)) == x for x without a Nyquist
- * component.  len: power of two, 32..4096.  Synchronous. */
+ * component.  len: power of two, 32..16384.  Synchronous. */
 MTB_API int32_t gpu_fft_real_inverse(const double *in_spec, int32_t len, double *out);
 
 /* Batch form: n_windows packed spectra in[w*window_len ...] -> samples. */

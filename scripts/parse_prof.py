@@ -13,7 +13,8 @@ import sys
 from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
-OURS = ("spectrum_kernel", "kalman_detrend_kernel")
+OURS = ("spectrum_kernel", "kalman_detrend_kernel", "inverse_kernel")
+MAIN = ("spectrum_kernel", "inverse_kernel")  # one per step; a Kalman pre-pass adds to its step
 
 
 def rows(pattern):
@@ -29,9 +30,12 @@ for r in rows("trace/**/*kernel_stats.csv"):
 
 
 def pmc(pattern, counter):
-    vals = [float(r["Counter_Value"]) for r in rows(pattern)
-            if r.get("Counter_Name") == counter and "spectrum_kernel" in r.get("Kernel_Name", "")]
-    return sum(vals) / len(vals) if vals else None
+    """Counter bytes per step: every dispatch of our kernels summed, divided by the number of
+    main-kernel dispatches (C3's Kalman pre-pass traffic belongs to the step it feeds)."""
+    rs = [r for r in rows(pattern) if r.get("Counter_Name") == counter]
+    vals = [float(r["Counter_Value"]) for r in rs if any(k in r.get("Kernel_Name", "") for k in OURS)]
+    n_main = sum(1 for r in rs if any(k in r.get("Kernel_Name", "") for k in MAIN))
+    return sum(vals) / n_main if n_main else None
 
 
 fetch = pmc("fetch/**/*counter_collection.csv", "FETCH_SIZE")
@@ -44,8 +48,9 @@ if write is not None:
     res["write_bytes"] = write * 1024
 if fetch is not None and write is not None:
     res["hbm_bytes_per_launch"] = res["read_bytes_corrected"] + res["write_bytes"]
-    res["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes, spectrum_kernel dispatches "
-                     "averaged; read = FETCH_SIZE*1024*2 (gfx950 half-count correction), write = WRITE_SIZE*1024")
+    res["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; all our kernels' dispatches "
+                     "summed per main (spectrum/inverse) dispatch; read = FETCH_SIZE*1024*2 (gfx950 half-count "
+                     "correction), write = WRITE_SIZE*1024")
 print(json.dumps(res, indent=1))
 tj = Path("profiles/traffic.json")
 allres = json.loads(tj.read_text()) if tj.exists() else {}

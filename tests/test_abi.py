@@ -69,7 +69,7 @@ def test_last_error_counts_terminator():
     assert L.gpu_get_last_error_w(small, 4) == 4 and small[3] == 0
 
 
-@pytest.mark.parametrize("n", [0, 16, 100, 8192])
+@pytest.mark.parametrize("n", [0, 16, 100, 8196, 32768])
 def test_bad_window_len(n):
     s = np.zeros(10000)
     out = np.zeros(10000)
@@ -85,7 +85,8 @@ def test_bad_modes_and_shapes():
     L = bridge.lib()
     got = C.c_int32(0)
     for args in ((1024, 1, 9, 1, 0, 0, 0), (1024, 1, 0, 7, 0, 0, 0), (1024, 1, 0, 1, 0, 5, 0),
-                 (1024, 0, 0, 1, 0, 0, 0), (8192, 1, 0, 1, 0, 0, 0)):
+                 (1024, 0, 0, 1, 0, 0, 0), (8192, 1, 0, 1, 0, 0, 0), (1024, 1, 0, 1, 0, 0, 5),
+                 (1024, 1, 0, 1, 0, 1, 3), (1024, 1, 0, 1, 0, 1, 4)):  # bad output; phase outputs are fp64
         n, hop, det, win, per, prec, outk = args
         st = L.gpu_spectrum_batch(bridge._dptr(s), s.size, n, hop, det, win, per, prec, outk, bridge._dptr(out),
                                   out.size, C.byref(got))

@@ -28,7 +28,7 @@ def ref(series, n, hop, detrend="none", window="hann", period=0, output="power")
     return oracle.batch_spectrum(series, n, hop, detrend, window, period, kalman=KALMAN, output=output)
 
 
-@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 def test_sizes_hann(gpu_session, n, prec):
     s = synth.random_walk(37 * n + 11, seed=n)
@@ -38,7 +38,7 @@ def test_sizes_hann(gpu_session, n, prec):
     assert oracle.rel_err(p, r) <= TOL[prec]
 
 
-@pytest.mark.parametrize("n", [64, 1024, 4096])
+@pytest.mark.parametrize("n", [64, 1024, 4096, 16384])
 @pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024), ("iir", 37), ("kalman", 0)])
 @pytest.mark.parametrize("window", ["none", "hann", "hamming", "blackman", "bartlett"])
 def test_detrend_window_matrix(gpu_session, n, detrend, period, window):
@@ -61,7 +61,8 @@ def test_f32_detrends(gpu_session, detrend, period):
     assert oracle.rel_err(p, ref(s32, n, n, detrend, "hann", period)) <= TOL["f32"]
 
 
-@pytest.mark.parametrize("n,hop", [(2048, 1), (1024, 3), (256, 1), (4096, 4097), (512, 700), (64, 1)])
+@pytest.mark.parametrize("n,hop", [(2048, 1), (1024, 3), (256, 1), (4096, 4097), (512, 700), (64, 1), (16384, 1),
+                                   (8192, 333)])
 def test_overlap_and_unaligned_hops(gpu_session, n, hop):
     """hop=1 (C4 shape, odd offsets -> unaligned loads), hop > N (gaps)."""
     s = synth.random_walk((150 - 1) * hop + n, seed=13)
@@ -79,7 +80,7 @@ def test_ragged_window_counts(gpu_session, nwin):
     assert oracle.rel_err(gpu(s, n, n, "mean"), ref(s, n, n, "mean")) <= TOL["f64"]
 
 
-@pytest.mark.parametrize("n", [32, 1024, 4096])
+@pytest.mark.parametrize("n", [32, 1024, 4096, 16384])
 def test_packed_output(gpu_session, n):
     s = synth.random_walk(5 * n, seed=5)
     p = gpu(s, n, n, "none", "hann", output="packed")
@@ -253,7 +254,8 @@ def _topk_match(got, want, tol, full_max):
 
 
 @pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),
-                                               (256, 256, 16, 2, 10000), (512, 512, 8, 300, 400)])
+                                               (256, 256, 16, 2, 10000), (512, 512, 8, 300, 400),
+                                               (16384, 16384, 8, 18, 52), (8192, 100, 64, 2, 8192)])
 @pytest.mark.parametrize("detrend", ["none", "iir"])
 def test_topk_scan(gpu_session, n, hop, k, minp, maxp, detrend):
     """Fused top-k bin scan (gpuopt-nodetrend.mq5:536-554) against the oracle."""
@@ -289,7 +291,7 @@ def _nyquist_free(x):
     return x - np.outer(x @ alt, alt).reshape(x.shape) / n
 
 
-@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384])
 def test_inverse_batch_vs_oracle(gpu_session, n):
     """gpu_fft_real_inverse_batch (L/WaveSpecZZ_1.0.4-core.mq5:65,426) on random packed spectra,
     ragged window count; bar: max |x - x_ref| <= 1e-12 * max |x_ref| (fp64 round-off of two FFTs)."""
@@ -302,7 +304,7 @@ def test_inverse_batch_vs_oracle(gpu_session, n):
         assert np.max(np.abs(got[i] - want)) <= 1e-12 * np.max(np.abs(want)), i
 
 
-@pytest.mark.parametrize("n", [32, 1024, 4096])
+@pytest.mark.parametrize("n", [32, 1024, 4096, 16384])
 def test_inverse_round_trip_single(gpu_session, n):
     """gpu_fft_real_inverse(gpu_fft_real_forward(x)) == x (x without a Nyquist component), the
     round trip ApplySpectralStages makes (core.mq5:344 -> :426)."""
@@ -369,7 +371,7 @@ def _delay_match(got, want, mag, m):
     assert np.all((np.abs(got - want) <= tn)[cond])
 
 
-@pytest.mark.parametrize("n", [32, 256, 1024, 4096])
+@pytest.mark.parametrize("n", [32, 256, 1024, 4096, 16384])
 @pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024)])
 def test_phase_output(gpu_session, n, detrend, period):
     """MTB_OUT_PHASE: [P | unwrapped phase | group delay] (1.0.4-new.mq5:1040-1120 at :3225-3227)."""
@@ -386,7 +388,8 @@ def test_phase_output(gpu_session, n, detrend, period):
         _delay_match(got[w, 2], want[w, 2], mag, m)
 
 
-@pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64)])
+@pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),
+                                               (16384, 4000, 8, 18, 52)])
 def test_topk_phase(gpu_session, n, hop, k, minp, maxp):
     """MTB_OUT_TOPK_PHASE: top-k records + unwrapped phase / group delay at each chosen bin (the
     values ComputeETA_RealFFT / CalculateScientificETASeconds read, 1.0.4-new.mq5:1165, :1239)."""
