@@ -232,6 +232,12 @@ int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int
         set_error("output=%d (phase) is computed in fp64 only", output);
         return MTB_BAD_ARGS;
     }
+    // the Kalman pre-pass addresses a 64-window tile with 32-bit offsets (kalman_core.h)
+    if (detrend == MTB_DETREND_KALMAN &&
+        (64 * hop + window_len) * (precision == MTB_PREC_F32 ? 4 : 8) >= (int64_t(1) << 31)) {
+        set_error("hop=%lld: the Kalman detrend needs 64 * hop samples within 2 GiB", (long long)hop);
+        return MTB_BAD_ARGS;
+    }
     c->n = window_len;
     c->log2n = l;
     c->hop = hop;
@@ -299,9 +305,9 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         K.n = c.n;
         K.f32 = c.f32;
         memcpy(K.params, kalman, sizeof(K.params));
-        static const int kvar = [] {  // tuning override: WSP_KALMAN_WPW=32|64 windows per wave
-            const char *e = getenv("WSP_KALMAN_WPW");
-            return e ? (atoi(e) == 32 ? 1 : atoi(e) == 64 ? 2 : 0) : 0;
+        static const int kvar = [] {  // ablation override: WSP_KALMAN_SPREAD=0 -> single-wave workgroups
+            const char *e = getenv("WSP_KALMAN_SPREAD");
+            return e && atoi(e) == 0 ? 1 : 0;
         }();
         K.variant = kvar;
         HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);

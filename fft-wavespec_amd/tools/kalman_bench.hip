@@ -1,0 +1,211 @@
+// kalman_bench.hip -- ablation and correctness probe of the Kalman detrend
+// pre-pass (not part of the library).  Built with -fno-slp-vectorize like
+// csrc/kalman_kernels.hip, so the timed code is the library's code.
+//
+//   kalman_bench time  [reps=10]   variants at C3 (65536 x 4096, f32), back to back
+//                                  and alternating with a 1.5 GB streaming kernel
+//                                  (the C3 step's spectrum launch in between)
+//   kalman_bench check             variants vs a host restatement of the reference step
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../csrc/kalman_core.h"
+
+using namespace wsp;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t err_ = (x);                                                                \
+        if (err_ != hipSuccess) {                                                             \
+            fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(err_), __FILE__, __LINE__); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+static const double kDefaults[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
+
+// launch one variant: WAVES = 4 adds the one-workgroup-per-CU LDS reservation
+template <typename T, int J, int FL, bool TWO, int WAVES>
+void launch(const T *x, T *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
+    const size_t reserve = WAVES == 4 ? 84 * 1024 - 4 * 64 * (J + 1) * sizeof(T) : 0;
+    hipLaunchKernelGGL((kcore::kalman_detrend_kernel<T, T, J, 64, J, FL, TWO, WAVES>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)),
+                       dim3(64 * WAVES), reserve, s, x, d, hop, W, n, kp);
+}
+
+__global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        out[j] = in[j];
+}
+
+template <int FL, bool TWO, int WAVES>
+void time_variant(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n,
+                  int reps, hipStream_t s) {
+    kcore::KP kp;
+    memcpy(&kp, kDefaults, sizeof(kp));
+    hipEvent_t a, b, c;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventCreate(&c));
+    launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+    CK(hipEventRecord(a, s));
+    for (int r = 0; r < reps; ++r) launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float back, alt = 0;
+    CK(hipEventElapsedTime(&back, a, b));
+    for (int r = 0; r < reps; ++r) {
+        hipLaunchKernelGGL(stream_copy, dim3(8192), dim3(256), 0, s, ci, co, cn);
+        CK(hipEventRecord(a, s));
+        launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+        CK(hipEventRecord(c, s));
+        CK(hipEventSynchronize(c));
+        float t;
+        CK(hipEventElapsedTime(&t, a, c));
+        alt += t;
+    }
+    printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us\n", name, back * 1e3f / reps, alt * 1e3f / reps);
+    fflush(stdout);
+}
+
+int time_main(int reps) {
+    const int64_t W = 65536;
+    const int n = 4096;
+    float *x, *d;
+    CK(hipMalloc(&x, W * n * 4));
+    CK(hipMalloc(&d, W * n * 4));
+    std::vector<float> h(W * n);
+    std::mt19937_64 rng(11);
+    std::normal_distribution<double> nd;
+    double v = 1.1;
+    for (int64_t i = 0; i < W * n; ++i) {  // synth.random_walk: 1.1 + cumsum(1e-4 N(0,1)) + 0.002 sin(2 pi t/50)
+        v += 1e-4 * nd(rng);
+        h[i] = (float)(v + 0.002 * sin(2 * M_PI * (double)i / 50));
+    }
+    CK(hipMemcpy(x, h.data(), W * n * 4, hipMemcpyHostToDevice));
+    const int64_t cn = (int64_t)768 << 20 >> 4;  // 768 MiB in, 768 MiB out
+    double2 *ci, *co;
+    CK(hipMalloc(&ci, cn * 16));
+    CK(hipMalloc(&co, cn * 16));
+    CK(hipMemset(ci, 0, cn * 16));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    for (int round = 0; round < 2; ++round) {
+        printf("round %d\n", round);
+        time_variant<kcore::kKfRuntime, true, 1>("1-wave WG, runtime flags, two-stage", x, d, ci, co, cn, W, n, reps, s);
+        time_variant<3, false, 1>("1-wave WG, static flags, expanded", x, d, ci, co, cn, W, n, reps, s);
+        time_variant<3, true, 1>("1-wave WG, static flags, two-stage", x, d, ci, co, cn, W, n, reps, s);
+        time_variant<3, true, 4>("4-wave WG + 1 WG/CU, static, two-stage", x, d, ci, co, cn, W, n, reps, s);
+        time_variant<kcore::kKfRuntime, true, 4>("4-wave WG + 1 WG/CU, runtime, two-stage", x, d, ci, co, cn, W, n, reps, s);
+    }
+    return 0;
+}
+
+// host restatement of ResetKalmanState / StepKalman4D
+// (L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:2015-2125), full 4x4 covariance
+static void host_kalman(const double *x, int n, const double *kp, double *d) {
+    const double q = fmax(0.05, kp[0]);
+    const double Qp = fmax(1e-9, kp[1] * q), Qv = fmax(1e-9, kp[2] * q), Qa = fmax(1e-9, kp[3] * q),
+                 Qj = fmax(1e-9, kp[4] * q), R = fmax(1e-9, kp[6]);
+    double pos = x[0], vel = kp[11], acc = kp[12], jerk = kp[13];
+    double P[4][4] = {{fmax(1e-9, kp[7]), 0, 0, 0}, {0, fmax(1e-9, kp[8]), 0, 0}, {0, 0, fmax(1e-9, kp[9]), 0},
+                      {0, 0, 0, fmax(1e-9, kp[10])}};
+    const double F[4][4] = {{1, 1, 0.5, 1.0 / 6.0}, {0, 1, 1, 0.5}, {0, 0, 1, 1}, {0, 0, 0, 1}};
+    double ema = 0;
+    bool ema_ready = false;
+    for (int j = 0; j < n; ++j) {
+        double x0p = pos + vel + 0.5 * acc + jerk / 6.0, x1p = vel + acc + 0.5 * jerk, x2p = acc + jerk, x3p = jerk;
+        double A[4][4] = {}, Pp[4][4] = {};
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                for (int k = 0; k < 4; ++k) A[a][b] += F[a][k] * P[k][b];
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                for (int k = 0; k < 4; ++k) Pp[a][b] += A[a][k] * F[b][k];
+        Pp[1][1] += P[1][2] + P[2][2] + 0.5 * (P[1][3] + P[2][3]);  // the reference's P11 (:2052)
+        Pp[0][0] += Qp; Pp[1][1] += Qv; Pp[2][2] += Qa; Pp[3][3] += Qj;
+        double y = x[j] - x0p, S = Pp[0][0] + R;
+        if (kp[5] > 0) {
+            double k = fmin(5.0, fabs(y) / sqrt(S)) * kp[5];
+            Pp[0][0] += k * Qp; Pp[1][1] += k * Qv; Pp[2][2] += k * Qa; Pp[3][3] += k * Qj;
+            S = Pp[0][0] + R;
+        }
+        if (kp[14] > 0) { double lim = kp[14] * sqrt(S); y = fmin(fmax(y, -lim), lim); }
+        double K[4];
+        for (int a = 0; a < 4; ++a) K[a] = Pp[a][0] / S;
+        pos = x0p + K[0] * y; vel = x1p + K[1] * y; acc = x2p + K[2] * y; jerk = x3p + K[3] * y;
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b) P[a][b] = Pp[a][b] - K[a] * Pp[0][b];
+        for (int a = 0; a < 4; ++a) P[a][a] = fmax(1e-12, P[a][a]);
+        double trend = pos;
+        if (kp[15] > 0) {
+            const double al = 2.0 / (kp[15] + 1.0);
+            if (!ema_ready) { ema = trend; ema_ready = true; }
+            ema = al * trend + (1.0 - al) * ema;
+            trend = ema;
+        }
+        d[j] = x[j] - trend;
+    }
+}
+
+template <int FL, bool TWO, int WAVES>
+void check_one(const char *name, const double *dx, double *dd, const std::vector<double> &ref, int64_t W, int64_t hop, int n,
+               const double *kpa) {
+    kcore::KP kp;
+    memcpy(&kp, kpa, sizeof(kp));
+    CK(hipMemset(dd, 0xff, (W + 300) * n * 8));  // NaN canary past the batch end as well
+    launch<double, 16, FL, TWO, WAVES>(dx, dd, hop, W, n, kp, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<double> h((W + 300) * n);
+    CK(hipMemcpy(h.data(), dd, h.size() * 8, hipMemcpyDeviceToHost));
+    double worst = 0;
+    int64_t at = -1;
+    for (int64_t i = 0; i < W * n; ++i) {
+        const double e = fabs(h[i] - ref[i]);
+        if (!(e <= worst)) { worst = e; at = i; }
+    }
+    int64_t touched = 0;  // stores past the batch end must be dropped
+    for (int64_t i = W * n; i < (int64_t)h.size(); ++i) touched += h[i] == h[i];
+    printf("%-40s max|d-ref| %.3e (window %lld step %lld)  writes past end: %lld\n", name, worst, (long long)(at / n),
+           (long long)(at % n), (long long)touched);
+}
+
+int check_main() {
+    const int64_t W = 100, hop = 37;
+    const int n = 256;
+    const int64_t len = (W - 1) * hop + n;
+    std::vector<double> x(len);
+    double v = 1.1;
+    for (int64_t i = 0; i < len; ++i) {
+        v += 1e-4 * (((i * 2654435761u) % 1000) / 500.0 - 1.0);
+        x[i] = v + 0.002 * sin(0.1256 * (double)i);
+    }
+    double *dx, *dd;
+    CK(hipMalloc(&dx, len * 8));
+    CK(hipMalloc(&dd, (W + 300) * n * 8));
+    CK(hipMemcpy(dx, x.data(), len * 8, hipMemcpyHostToDevice));
+    std::vector<double> ref(W * n);
+    for (int64_t w = 0; w < W; ++w) host_kalman(&x[w * hop], n, kDefaults, &ref[w * n]);
+    check_one<kcore::kKfRuntime, false, 1>("1-wave runtime expanded", dx, dd, ref, W, hop, n, kDefaults);
+    check_one<kcore::kKfRuntime, true, 1>("1-wave runtime two-stage", dx, dd, ref, W, hop, n, kDefaults);
+    check_one<3, true, 1>("1-wave static two-stage", dx, dd, ref, W, hop, n, kDefaults);
+    check_one<3, true, 4>("4-wave static two-stage", dx, dd, ref, W, hop, n, kDefaults);
+    double ema[16];
+    memcpy(ema, kDefaults, sizeof(ema));
+    ema[15] = 12.0;
+    for (int64_t w = 0; w < W; ++w) host_kalman(&x[w * hop], n, ema, &ref[w * n]);
+    check_one<kcore::kKfRuntime, true, 4>("4-wave runtime two-stage, EMA 12", dx, dd, ref, W, hop, n, ema);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    const std::string mode = argc > 1 ? argv[1] : "time";
+    if (mode == "check") return check_main();
+    return time_main(argc > 2 ? atoi(argv[2]) : 10);
+}

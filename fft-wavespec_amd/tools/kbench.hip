@@ -9,10 +9,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
-#include "../csrc/kalman_core.h"
 #include "../csrc/spectrum_dispatch.h"
 
 using namespace wsp;
@@ -96,53 +97,6 @@ float time_variant(const SpectrumLaunch &L, hipStream_t s, int reps) {
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
     return ms * 1000.f / reps;
-}
-
-template <int J, int WPW, int UNROLL>
-float time_kalman(const float *x, float *d, int64_t W, int n, int reps, hipStream_t s) {
-    kcore::KP kp{1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
-    const unsigned grid = (unsigned)((W + WPW - 1) / WPW);
-    auto go = [&] {
-        hipLaunchKernelGGL((kcore::kalman_detrend_kernel<float, float, J, WPW, UNROLL>), dim3(grid), dim3(64), 0, s, x,
-                           d, (int64_t)n, W, n, kp);
-    };
-    go();
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
-    CK(hipEventRecord(e0, s));
-    for (int i = 0; i < reps; ++i) go();
-    CK(hipEventRecord(e1, s));
-    CK(hipEventSynchronize(e1));
-    float ms;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    return ms * 1000.f / reps;
-}
-
-int kalman_main(int reps) {
-    const int64_t W = 65536;
-    const int n = 4096;
-    float *x, *d;
-    CK(hipMalloc(&x, W * n * 4));
-    CK(hipMalloc(&d, W * n * 4));
-    std::vector<float> h(W * n);
-    double v = 1.1;
-    for (int64_t i = 0; i < W * n; ++i) {
-        v += 1e-4 * (((i * 2654435761u) % 1000) / 500.0 - 1.0);
-        h[i] = (float)v;
-    }
-    CK(hipMemcpy(x, h.data(), W * n * 4, hipMemcpyHostToDevice));
-    hipStream_t s;
-    CK(hipStreamCreate(&s));
-    for (int round = 0; round < 2; ++round) {
-        printf("round %d kalman J=32 WPW=64 unroll=2   %9.1f us\n", round, time_kalman<32, 64, 2>(x, d, W, n, reps, s));
-        printf("round %d kalman J=32 WPW=64 unroll=32  %9.1f us\n", round, time_kalman<32, 64, 32>(x, d, W, n, reps, s));
-        printf("round %d kalman J=16 WPW=64 unroll=16  %9.1f us\n", round, time_kalman<16, 64, 16>(x, d, W, n, reps, s));
-        printf("round %d kalman J=32 WPW=64 unroll=1   %9.1f us\n", round, time_kalman<32, 64, 1>(x, d, W, n, reps, s));
-        printf("round %d kalman J=32 WPW=32 unroll=32  %9.1f us\n", round, time_kalman<32, 32, 32>(x, d, W, n, reps, s));
-        fflush(stdout);
-    }
-    return 0;
 }
 
 template <int OUT, int VAR>
@@ -254,8 +208,8 @@ int c4_main(int reps) {
     return 0;
 }
 
+
 int main(int argc, char **argv) {
-    if (argc > 1 && std::string(argv[1]) == "kalman") return kalman_main(argc > 2 ? atoi(argv[2]) : 5);
     if (argc > 1 && std::string(argv[1]) == "c4") return c4_main(argc > 2 ? atoi(argv[2]) : 5);
     if (argc > 1 && std::string(argv[1]) == "out") return out_main(argc > 2 ? atoi(argv[2]) : 20);
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;

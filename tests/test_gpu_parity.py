@@ -439,3 +439,41 @@ def test_phase_plan_and_bad_precision(gpu_session):
     plan.close()
     with pytest.raises(bridge.BridgeError):
         bridge.spectrum_batch(s[: 4 * n], n, n, "none", "hann", 0, "f32", "phase")
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("nwin,hop", [(1, 256), (63, 256), (65, 256), (130, 256), (200, 1), (150, 37)])
+def test_kalman_ragged_and_overlap(gpu_session, prec, nwin, hop):
+    """Kalman pre-pass: partial last 64-window tile (range-checked buffer IO), overlapping windows."""
+    n = 256
+    s = synth.random_walk((nwin - 1) * hop + n, seed=nwin + hop)
+    p = gpu(s, n, hop, "kalman", "hann", prec=prec)
+    r = ref(s.astype(np.float32).astype(np.float64) if prec == "f32" else s, n, hop, "kalman", "hann")
+    assert p.shape == r.shape == (nwin, n // 2)
+    assert oracle.rel_err(p, r) <= TOL[prec]
+
+
+def _kp(**kw):
+    names = ["follow", "qp", "qv", "qa", "qj", "adapt", "r", "vp", "vv", "va", "vj", "iv", "ia", "ij", "clip", "ema"]
+    p = list(KALMAN)
+    for k, v in kw.items():
+        p[names.index(k)] = v
+    return p
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("kw", [dict(ema=20.0), dict(adapt=0.0), dict(clip=0.0), dict(adapt=0.0, clip=0.0, ema=5.0),
+                                dict(follow=2.5, iv=1e-4, ia=-1e-6)])
+def test_kalman_params(gpu_session, prec, kw):
+    """gpu_set_kalman_params: non-default flags take the runtime-flag kernel (kalman_kernels.hip)."""
+    kp = _kp(**kw)
+    n = 1024
+    s = synth.random_walk(70 * n, seed=5)
+    bridge.set_kalman_params(kp)
+    try:
+        p = gpu(s, n, n, "kalman", "hann", prec=prec)
+    finally:
+        bridge.set_kalman_params(KALMAN)
+    s_ref = s.astype(np.float32).astype(np.float64) if prec == "f32" else s
+    r = oracle.batch_spectrum(s_ref, n, n, "kalman", "hann", 0, kalman=kp)
+    assert oracle.rel_err(p, r) <= TOL[prec], kw
