@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="north_star",
-                    choices=["c2", "c3", "north_star", "c4", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse"])
+                    choices=["c2", "c3", "north_star", "c4", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse", "large",
+                             "large_262144"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()

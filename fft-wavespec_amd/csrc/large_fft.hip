@@ -1,0 +1,535 @@
+// large_fft.hip -- windows of N = 32768 .. 262144 samples (SURVEY 8f rank 4:
+// the legacy InpFFTWindow menu up to 262144, default 65536 in
+// L/WaveSpecZZ_1.0.4-new.mq5:657).
+//
+// One window no longer fits a workgroup (M = N/2 complex points = 256 KiB ..
+// 2 MiB), so the M-point complex FFT of z[n] = x[2n] + i x[2n+1] runs as a
+// four-step transform, M = M1 x M2, n = n1 + M1 n2, k = k2 + M2 k1:
+//
+//   col_kernel  per window and block of CB consecutive n1: gather the column
+//               z[n1 + M1 n2] (CB x 16 B contiguous per row), detrend (mean)
+//               + window on load, M2-point FFT over n2, twiddle W_M^(n1 k2),
+//               store Y[k2][n1] (rows of M1 complex).
+//   row_kernel  per window and block of RB rows k2 plus their mirror rows
+//               M2 - k2: M1-point FFT of each row -> Z[k2 + M2 k1]; the real
+//               post-processing pairs Z[k] with Z[M - k], which sits in the
+//               mirror row of the same workgroup (row 0 and row M2/2 pair
+//               with themselves); |X_k|^2 or the packed (Re, Im) layout,
+//               staged through LDS so that each row block leaves as runs of
+//               RB consecutive bins.
+//
+// Y for a chunk of windows (about 192 MiB: the measured optimum between
+// launch count and Infinity-Cache residency) is written and read back right
+// away.  Each workgroup walks several windows of the chunk with a register
+// prefetch of the next window's slice.  Both kernels share one workgroup FFT: 16
+// complex points per thread, L/16 threads per transform, Stockham passes
+// of radix 16 (and one of 2/4/8), LDS between passes (+1 pad per 16), and
+// the twiddles of every pass from the W_N table.
+//
+// Detrend: mean by a per-window reduction pre-pass (mean_kernel), IIR trend
+// by a per-window scan pre-pass (iir_kernel, restarts per window as
+// L/WaveSpecZZ_1.0.2.mq5:3040-3053), Kalman by the common pre-pass; the
+// latter two write detrended windows that the column pass reads with hop = N.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+#include "spectrum_dispatch.h"
+
+namespace wsp {
+namespace large {
+
+using core::cadd;
+using core::cconj;
+using core::cmul;
+using core::cpx;
+using core::csub;
+using core::dft;
+using core::pad16;
+
+template <int LOG2L> struct LGeo {
+    static constexpr int L = 1 << LOG2L;
+    static constexpr int TP = L / 16;                         // threads per transform
+    static constexpr int NP = LOG2L / 4 + (LOG2L % 4 ? 1 : 0);  // passes
+    static constexpr int radix(int p) { return p < LOG2L / 4 ? 16 : (1 << (LOG2L % 4)); }
+    static constexpr int ns(int p) {
+        int s = 1;
+        for (int i = 0; i < p; ++i) s *= radix(i);
+        return s;
+    }
+    static constexpr int SLOT = L + L / 16;  // padded LDS elements per transform
+    static_assert(LOG2L >= 6 && LOG2L <= 9, "transform length 64 .. 512");
+};
+
+// L-point forward FFT of one transform held by TP threads (16 points each:
+// v[r] = x[t + TP r] on entry).  On exit v[q R + r] = X[b + (L/R) r] with
+// b = t + TP q and R the last pass's radix.  `slot` is this transform's LDS
+// region (SLOT elements); tw = W_N^j, j < N, of a table of period N (twN).
+template <typename T, int LOG2L, int PASS = 1>
+__device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, const cpx<T> *__restrict__ tw, int log2tw) {
+    using G = LGeo<LOG2L>;
+    constexpr int L = G::L, TP = G::TP;
+    if constexpr (PASS == 1) dft<T, 16>(v);  // pass 0: radix 16 over r, no twiddles (Ns = 1)
+    if constexpr (PASS < G::NP) {
+        // write the previous pass's outputs: butterfly b (Ns = ns(PASS-1), R = radix(PASS-1))
+        constexpr int Rp = G::radix(PASS - 1), Nsp = G::ns(PASS - 1);
+#pragma unroll
+        for (int q = 0; q < 16 / Rp; ++q) {
+            const int b = t + TP * q, j = b % Nsp, base = (b / Nsp) * Nsp * Rp + j;
+#pragma unroll
+            for (int r = 0; r < Rp; ++r) slot[pad16(base + Nsp * r)] = v[q * Rp + r];
+        }
+        __syncthreads();
+        constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q) {
+            const int b = t + TP * q, j = b % Ns;
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[q * R + r] = slot[pad16(b + (L / R) * r)];
+            // twiddle W_{Ns R}^{j r} = W_N^{j r N/(Ns R)}: one table entry, powers by products
+            // (<= 15 steps: ~15 ulp)
+            const cpx<T> w1 = tw[(j << log2tw) / (Ns * R)];
+            cpx<T> wr = w1;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                v[q * R + r] = cmul(v[q * R + r], wr);
+                if (r + 1 < R) wr = cmul(wr, w1);
+            }
+            dft<T, R>(v + q * R);
+        }
+        __syncthreads();  // slot reuse by the caller / next pass
+        wg_fft<T, LOG2L, PASS + 1>(v, slot, t, tw, log2tw);
+    }
+}
+
+template <int LOG2L> __device__ __forceinline__ constexpr int last_radix() { return LGeo<LOG2L>::radix(LGeo<LOG2L>::NP - 1); }
+
+struct ColArgs {
+    const void *series;  // window w at series + w*hop
+    void *y;             // chunk rows: Y[wc][k2][n1]
+    const void *tw;      // W_N^k, k < N
+    const double *means; // per window (mean detrend) or null
+    int64_t hop, w0, nwin;  // windows w0 .. w0 + nwin - 1 of this chunk
+    int log2n, vec;
+    double a0, a1, a2, cd, sd, c1, s1, inv_theta, inv_nm1;  // window: rotation by th*2*M1*TP per r, th per odd sample
+};
+
+constexpr int kCB = 16;  // columns per workgroup in col_kernel
+
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN>
+__global__ __launch_bounds__(kCB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) {
+    using G = LGeo<LOG2M2>;
+    constexpr int M1 = 1 << LOG2M1, M2 = G::L, TP = G::TP, NB1 = M1 / kCB;
+    constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
+    __shared__ cpx<T> lds[kCB * G::SLOT];
+    const int tid = threadIdx.x, c = tid % kCB, t = tid / kCB;
+    const int beta = blockIdx.x % NB1;
+    const int n1 = beta * kCB + c;
+    const T *__restrict__ series = static_cast<const T *>(a.series);
+    const cpx<T> *__restrict__ tw = static_cast<const cpx<T> *>(a.tw);
+    cpx<T> *__restrict__ y = static_cast<cpx<T> *>(a.y);
+    const int N = 1 << a.log2n;
+    // window angle of sample 2n at r = 0: th * 2 (n1 + M1 t); per r: + th * 2 M1 TP
+    double cw0 = 1.0, sw0 = 0.0;
+    if constexpr (kCos) sincos(a.inv_theta * (double)(2 * (n1 + M1 * t)), &sw0, &cw0);
+    using v2 = typename core::V2<T>::t;
+    v2 raw[16];
+    auto load = [&](int64_t wc) {  // the 16 sample pairs of this thread's column slice of window w0 + wc
+        const T *__restrict__ xw = series + (a.w0 + wc) * a.hop;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = n1 + M1 * (t + TP * r);
+            if (a.vec) {
+                raw[r] = __builtin_nontemporal_load(reinterpret_cast<const v2 *>(xw + 2 * n));
+            } else {
+                raw[r].x = xw[2 * n];
+                raw[r].y = xw[2 * n + 1];
+            }
+        }
+    };
+    // register prefetch of the next window (64 VGPRs in fp64) except at M2 = 512, whose
+    // 512-thread workgroup has only 256 VGPRs per lane
+    constexpr bool kPrefetch = LOG2M2 < 9 || sizeof(T) == 4;
+    const int64_t wstep = gridDim.x / NB1;
+    int64_t wc = blockIdx.x / NB1;
+    if (kPrefetch && wc < a.nwin) load(wc);
+    for (; wc < a.nwin; wc += wstep) {
+        if (!kPrefetch) load(wc);
+        const double mean = MEAN ? a.means[a.w0 + wc] : 0.0;
+        cpx<T> v[16];
+        double cw = cw0, sw = sw0;
+        if constexpr (kCos) asm volatile("" : "+v"(cw), "+v"(sw));
+        int nb = n1 + M1 * t;  // sample pair index of r = 0, advanced per r (pinned: no 16-value hoist)
+        if constexpr (WCLASS == core::kWinBartlett) asm volatile("" : "+v"(nb));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = nb + M1 * TP * r;
+            double xa = (double)raw[r].x, xb = (double)raw[r].y;
+            if constexpr (MEAN) {
+                xa -= mean;
+                xb -= mean;
+            }
+            if constexpr (kCos) {
+                const double co = cw * a.c1 - sw * a.s1;  // odd sample: th + th1
+                if constexpr (WCLASS == core::kWinCos2) {
+                    xa *= a.a0 + a.a1 * cw + a.a2 * (2.0 * cw * cw - 1.0);
+                    xb *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                } else {
+                    xa *= a.a0 + a.a1 * cw;
+                    xb *= a.a0 + a.a1 * co;
+                }
+                const double cn = cw * a.cd - sw * a.sd;
+                sw = sw * a.cd + cw * a.sd;
+                cw = cn;
+            } else if constexpr (WCLASS == core::kWinBartlett) {  // L/WaveSpecZZ_1.0.2.mq5:918-922
+                xa *= 1.0 - fabs((2.0 * (2 * n) - N + 1) * a.inv_nm1);
+                xb *= 1.0 - fabs((2.0 * (2 * n + 1) - N + 1) * a.inv_nm1);
+            }
+            v[r] = {(T)xa, (T)xb};
+        }
+        if (kPrefetch && wc + wstep < a.nwin) load(wc + wstep);  // next window's samples in flight during this FFT
+        wg_fft<T, LOG2M2>(v, lds + c * G::SLOT, t, tw, a.log2n);
+        // v[q R + r] = X[k2], k2 = t + TP q + (M2/R) r; twiddle W_M^(n1 k2) = W_N^(2 n1 k2)
+        constexpr int R = last_radix<LOG2M2>();
+        cpx<T> *__restrict__ yw = y + wc * (int64_t)M2 * M1;
+        const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q) {
+            cpx<T> wr = tw[(2 * n1 * (t + TP * q)) & (N - 1)];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int k2 = t + TP * q + (M2 / R) * r;
+                yw[(int64_t)k2 * M1 + n1] = cmul(v[q * R + r], wr);
+                if (r + 1 < R) wr = cmul(wr, wstep_r);
+            }
+        }
+    }
+}
+
+struct RowArgs {
+    const void *y;   // Y[wc][k2][n1]
+    void *out;       // window w's record at out + w * record
+    const void *tw;  // W_N^k
+    int64_t w0, nwin;
+    int log2n;
+    int packed;      // 0: |X_k|^2 (N/2 per window); 1: out[2k] = Re X_k, out[2k+1] = Im X_k (N per window)
+};
+
+template <int LOG2M1> struct RowGeo {
+    static constexpr int RB = LOG2M1 >= 8 ? 8 : 16;  // rows (and mirror rows) per workgroup
+};
+
+template <typename T, int LOG2M1, int LOG2M2, bool PACKED>
+__global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void row_kernel(RowArgs a) {
+    using G = LGeo<LOG2M1>;
+    constexpr int RB = RowGeo<LOG2M1>::RB;
+    constexpr int M1 = G::L, M2 = 1 << LOG2M2, TP = G::TP, NB2 = (M2 / 2) / RB;
+    constexpr int64_t M = (int64_t)M1 * M2;
+    __shared__ cpx<T> lds[2 * RB * G::SLOT];
+    const int tid = threadIdx.x, rho = tid / TP, t = tid % TP;
+    const int beta = blockIdx.x % NB2;
+    // slot rho < RB: row beta*RB + rho; slot RB + i: row M2 - (beta*RB + i), or M2/2 for i = 0 of block 0
+    auto row_of = [&](int s) {
+        const int i = s < RB ? s : s - RB, lo = beta * RB + i;
+        return s < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
+    };
+    const int row = row_of(rho);
+    const cpx<T> *__restrict__ tw = static_cast<const cpx<T> *>(a.tw);
+    const int N = 1 << a.log2n;
+    cpx<T> *slot = lds + rho * G::SLOT;
+    const int64_t wstep = gridDim.x / NB2;
+    int64_t wc = blockIdx.x / NB2;
+    cpx<T> nxt[16];
+    auto load = [&](int64_t w) {
+        const cpx<T> *__restrict__ yr = static_cast<const cpx<T> *>(a.y) + (w * M2 + row) * (int64_t)M1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[r] = yr[t + TP * r];
+    };
+    if (wc < a.nwin) load(wc);
+    for (; wc < a.nwin; wc += wstep) {
+        cpx<T> v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = nxt[r];
+        if (wc + wstep < a.nwin) load(wc + wstep);  // next window's rows in flight during this one
+        wg_fft<T, LOG2M1>(v, slot, t, tw, a.log2n);
+        // Z[row + M2 k1] in v[q R + r], k1 = t + TP q + (M1/R) r: to LDS in natural order
+        constexpr int R = last_radix<LOG2M1>();
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) slot[pad16(t + TP * q + (M1 / R) * r)] = v[q * R + r];
+        __syncthreads();
+        // X[k] = E + W_N^k O, E = (Z_k + conj Z_{M-k})/2, O = (Z_k - conj Z_{M-k})/(2i)
+        const bool self = row == 0 || row == M2 / 2;
+        const cpx<T> *pslot = lds + (self ? rho : (rho < RB ? rho + RB : rho - RB)) * G::SLOT;
+        T res[16][PACKED ? 2 : 1];
+        const cpx<T> wstep_r = tw[(M2 * (M1 / R)) & (N - 1)];  // W_N^k along r: k += M2 M1/R
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q) {
+            cpx<T> wk = tw[(row + M2 * (t + TP * q)) & (N - 1)];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int k1 = t + TP * q + (M1 / R) * r;
+                const int pk1 = row == 0 ? ((M1 - k1) & (M1 - 1)) : (M1 - 1 - k1);
+                const cpx<T> z = v[q * R + r], zp = cconj(pslot[pad16(pk1)]);
+                const cpx<T> e = {T(0.5) * (z.re + zp.re), T(0.5) * (z.im + zp.im)};
+                const cpx<T> d = {T(0.5) * (z.re - zp.re), T(0.5) * (z.im - zp.im)};
+                const cpx<T> o = {d.im, -d.re};  // d / i
+                const cpx<T> x = cadd(e, cmul(wk, o));
+                if (r + 1 < R) wk = cmul(wk, wstep_r);
+                if constexpr (PACKED) {
+                    res[q * R + r][0] = x.re;
+                    res[q * R + r][1] = x.im;
+                } else {
+                    res[q * R + r][0] = x.re * x.re + x.im * x.im;
+                }
+            }
+        }
+        __syncthreads();  // partner reads done: the LDS becomes the output stage [k1][slot]
+        constexpr int E = PACKED ? 2 : 1;
+        T *stage = reinterpret_cast<T *>(lds);  // (M1 x 2RB) records of E values
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int k1 = t + TP * q + (M1 / R) * r;
+#pragma unroll
+                for (int e = 0; e < E; ++e) stage[(k1 * (2 * RB + 1) + rho) * E + e] = res[q * R + r][e];
+            }
+        __syncthreads();
+        // runs of RB consecutive bins per (k1, half): lanes over slots
+        T *__restrict__ ow = static_cast<T *>(a.out) + (a.w0 + wc) * (int64_t)(PACKED ? 2 * M : M);
+        constexpr int NT = 2 * RB * TP;
+        for (int i = tid; i < M1 * 2 * RB; i += NT) {
+            const int s = i % (2 * RB), k1 = i / (2 * RB);
+            const int64_t k = row_of(s) + (int64_t)M2 * k1;
+#pragma unroll
+            for (int e = 0; e < E; ++e) ow[k * E + e] = stage[(k1 * (2 * RB + 1) + s) * E + e];
+        }
+        __syncthreads();  // stage reads done before the next window's FFT
+    }
+}
+
+// ---------------------------------------------------------------- pre-passes
+
+// Per-window mean (L/WaveSpecZZ_gpu_wip.mq5:940-950) for the column pass.
+template <typename T>
+__global__ __launch_bounds__(256) void mean_kernel(const T *__restrict__ series, int64_t hop, int64_t n_windows, int n,
+                                                   double *__restrict__ means) {
+    __shared__ double red[4];
+    for (int64_t w = blockIdx.x; w < n_windows; w += gridDim.x) {
+        const T *__restrict__ xw = series + w * hop;
+        double s = 0.0;
+        for (int i = threadIdx.x; i < n; i += 256) s += (double)xw[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) means[w] = (red[0] + red[1] + red[2] + red[3]) / (double)n;
+        __syncthreads();
+    }
+}
+
+// Per-window IIR trend detrend (L/WaveSpecZZ_1.0.2.mq5:3040-3053, restarting
+// at every window): t0 = c (x0 + x0), tj = c (xj + x(j-1)) + alpha t(j-1),
+// d = x - t.  1024 threads per window, C = N/1024 consecutive samples each:
+// local filter from a zero state, affine carry scan across threads
+// (multipliers apow[j] = alpha^(C 2^j)), then the chunk again with its carry.
+struct IirPow {
+    double alpha, c;
+    double apow[8];  // alpha^(C 2^j), C = N/1024 samples per thread
+};
+
+template <typename T>
+__global__ __launch_bounds__(1024) void iir_kernel(const T *__restrict__ series, int64_t hop, int64_t n_windows, int n,
+                                                  IirPow ip, T *__restrict__ dout) {
+    __shared__ double wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double alpha = ip.alpha, c = ip.c;
+    const double *apow = ip.apow;
+    const int C = n / 1024;
+    for (int64_t w = blockIdx.x; w < n_windows; w += gridDim.x) {
+        const T *__restrict__ xw = series + w * hop;
+        const int j0 = tid * C;
+        double prev = (double)xw[j0 == 0 ? 0 : j0 - 1];
+        double tr = 0.0;
+        for (int j = 0; j < C; ++j) {
+            const double x = (double)xw[j0 + j];
+            tr = c * (x + prev) + alpha * tr;
+            prev = x;
+        }
+        // inclusive scan of (A = alpha^C, tr) within the wave, then across the 16 waves
+        double v = tr;
+#pragma unroll
+        for (int k = 0, d = 1; d < 64; ++k, d <<= 1) {
+            const double up = __shfl_up(v, d, 64);
+            if (lane >= d) v = apow[k] * up + v;
+        }
+        if (lane == 63) wsum[wv] = v;
+        __syncthreads();
+        double G = 0.0;  // state entering this wave: sum over earlier waves, apow[6] = alpha^(64 C)
+        for (int i = 0; i < wv; ++i) G = apow[6] * G + wsum[i];
+        // carry into this thread = state after the previous chunk
+        double carry = __shfl_up(v, 1, 64);
+        double p = 1.0;  // alpha^(C lane)
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if ((lane >> k) & 1) p *= apow[k];
+        carry = lane == 0 ? G : carry + p * G;
+        if (tid == 0) carry = 0.0;
+        __syncthreads();  // wsum reuse
+        tr = carry;
+        prev = (double)xw[j0 == 0 ? 0 : j0 - 1];
+        T *__restrict__ dw = dout + w * (int64_t)n;
+        for (int j = 0; j < C; ++j) {
+            const double x = (double)xw[j0 + j];
+            tr = c * (x + prev) + alpha * tr;
+            prev = x;
+            dw[j0 + j] = (T)(x - tr);
+        }
+    }
+}
+
+}  // namespace large
+
+// ------------------------------------------------------------------- launch
+namespace {
+
+int cu_count() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return n > 0 ? n : 256;
+    }();
+    return cus;
+}
+
+// windows in flight: enough workgroups for every CU's LDS (two per CU at
+// 70 KiB), each walking several windows of the chunk with a prefetch
+int64_t windows_in_flight(int64_t nwin, int blocks_per_window, size_t lds_bytes) {
+    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / (int64_t)lds_bytes);
+    const int64_t slots = per_cu * cu_count();
+    return std::max<int64_t>(1, std::min<int64_t>(nwin, slots / blocks_per_window));
+}
+
+template <typename T, int LM1, int LM2, int WC, bool MEAN>
+hipError_t col_launch(const large::ColArgs &a, hipStream_t s) {
+    constexpr int NB1 = (1 << LM1) / large::kCB;
+    const int64_t g = windows_in_flight(a.nwin, NB1, large::kCB * large::LGeo<LM2>::SLOT * sizeof(core::cpx<T>)) * NB1;
+    hipLaunchKernelGGL((large::col_kernel<T, LM1, LM2, WC, MEAN>), dim3((unsigned)g), dim3(large::kCB * (1 << LM2) / 16), 0,
+                       s, a);
+    return hipGetLastError();
+}
+
+template <typename T, int LM1, int LM2, bool PACKED> hipError_t row_launch(const large::RowArgs &a, hipStream_t s) {
+    constexpr int RB = large::RowGeo<LM1>::RB, NB2 = ((1 << LM2) / 2) / RB;
+    const int64_t g = windows_in_flight(a.nwin, NB2, 2 * RB * large::LGeo<LM1>::SLOT * sizeof(core::cpx<T>)) * NB2;
+    hipLaunchKernelGGL((large::row_kernel<T, LM1, LM2, PACKED>), dim3((unsigned)g), dim3(2 * RB * (1 << LM1) / 16), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunch &L, const large::ColArgs &ca,
+                                                                const large::RowArgs &ra, int wclass, bool mean,
+                                                                hipStream_t s) {
+    hipError_t e;
+    using namespace core;
+#define COL(WC)                                                                            \
+    e = mean ? col_launch<T, LM1, LM2, WC, true>(ca, s) : col_launch<T, LM1, LM2, WC, false>(ca, s)
+    switch (wclass) {
+    case kWinCos: COL(kWinCos); break;
+    case kWinCos2: COL(kWinCos2); break;
+    case kWinBartlett: COL(kWinBartlett); break;
+    default: COL(kWinNone); break;
+    }
+#undef COL
+    if (e != hipSuccess) return e;
+    return L.packed ? row_launch<T, LM1, LM2, true>(ra, s) : row_launch<T, LM1, LM2, false>(ra, s);
+}
+
+template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
+    const int log2m = L.log2n - 1;
+    const int n = 1 << L.log2n;
+    // pre-passes
+    const void *src = L.series;
+    int64_t hop = L.hop;
+    const double *means = nullptr;
+    if (L.detrend == kDetrendMean) {
+        hipLaunchKernelGGL(large::mean_kernel<T>, dim3((unsigned)std::min<int64_t>(L.n_windows, 4096)), dim3(256), 0, s,
+                           static_cast<const T *>(L.series), L.hop, L.n_windows, n, L.means);
+        means = L.means;
+    } else if (L.detrend == kDetrendIir) {
+        large::IirPow ip{};
+        ip.alpha = L.iir_alpha;
+        ip.c = L.iir_c;
+        long double pw = powl((long double)L.iir_alpha, (long double)(n / 1024));
+        for (int j = 0; j < 8; ++j) {
+            ip.apow[j] = (double)pw;
+            pw = pw * pw;
+        }
+        hipLaunchKernelGGL(large::iir_kernel<T>, dim3((unsigned)std::min<int64_t>(L.n_windows, 1024)), dim3(1024), 0, s,
+                           static_cast<const T *>(L.series), L.hop, L.n_windows, n, ip, static_cast<T *>(L.detrended));
+        src = L.detrended;
+        hop = n;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    large::ColArgs ca{};
+    ca.series = src;
+    ca.y = L.y;
+    ca.tw = L.twiddle;
+    ca.means = means;
+    ca.hop = hop;
+    ca.log2n = L.log2n;
+    ca.vec = (hop % 2 == 0) && (reinterpret_cast<uintptr_t>(src) % (2 * sizeof(T)) == 0);
+    const int wclass = core::window_class(L.window, &ca.a0, &ca.a1, &ca.a2);
+    const int lm1 = log2m / 2, lm2 = log2m - lm1;  // M1 <= M2: the column pass takes the longer transform
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    const long double th = two_pi / (long double)(n - 1);
+    ca.inv_theta = (double)th;
+    ca.inv_nm1 = 1.0 / (double)(n - 1);
+    const long double dstep = th * 2.0L * (long double)(1 << lm1) * (long double)((1 << lm2) / 16);
+    ca.cd = (double)cosl(dstep);
+    ca.sd = (double)sinl(dstep);
+    ca.c1 = (double)cosl(th);
+    ca.s1 = (double)sinl(th);
+    large::RowArgs ra{};
+    ra.y = L.y;
+    ra.out = L.out;
+    ra.tw = L.twiddle;
+    ra.log2n = L.log2n;
+    ra.packed = L.packed;
+    for (int64_t w0 = 0; w0 < L.n_windows; w0 += L.chunk) {
+        ca.w0 = ra.w0 = w0;
+        ca.nwin = ra.nwin = std::min<int64_t>(L.chunk, L.n_windows - w0);
+        switch (log2m) {
+        case 14: e = chunk_launch<T, 7, 7>(L, ca, ra, wclass, means != nullptr, s); break;
+        case 15: e = chunk_launch<T, 7, 8>(L, ca, ra, wclass, means != nullptr, s); break;
+        case 16: e = chunk_launch<T, 8, 8>(L, ca, ra, wclass, means != nullptr, s); break;
+        case 17: e = chunk_launch<T, 8, 9>(L, ca, ra, wclass, means != nullptr, s); break;
+        default: return hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+int64_t large_chunk(int log2n, bool f32) {
+    static const int64_t mb = [] {
+        const char *e = getenv("WSP_LARGE_CHUNK_MB");
+        const int64_t v = e ? atoll(e) : 0;
+        return v > 0 ? v : int64_t(192);
+    }();
+    const int64_t per = (int64_t(1) << (log2n - 1)) * (f32 ? 8 : 16);
+    const int64_t c = (mb << 20) / per;
+    return c < 1 ? 1 : c;
+}
+
+hipError_t launch_large(const LargeLaunch &L, hipStream_t stream) {
+    if (L.n_windows <= 0) return hipSuccess;
+    return L.f32 ? launch_t<float>(L, stream) : launch_t<double>(L, stream);
+}
+
+}  // namespace wsp

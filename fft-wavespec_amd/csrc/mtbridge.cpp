@@ -209,13 +209,38 @@ int ilog2_exact(int n) {
     return l;
 }
 
+// Device workspace of one launch: [detrended windows][per-window means][chunk column results]
+struct WsLayout {
+    size_t det = 0, means = 0, y = 0, total = 0;
+};
+size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+WsLayout ws_layout(const Config &c) {
+    WsLayout L;
+    const size_t es = c.elem();
+    const bool large = c.op == kOpSpectrum && c.log2n > kMaxLog2N;
+    size_t det = 0, means = 0, y = 0;
+    if (c.op == kOpSpectrum && (c.detrend == MTB_DETREND_KALMAN || (large && c.detrend == MTB_DETREND_IIR)))
+        det = (size_t)(c.n_windows * c.n) * es;
+    if (large && c.detrend == MTB_DETREND_MEAN) means = (size_t)c.n_windows * sizeof(double);
+    if (large) y = (size_t)std::min<int64_t>(c.n_windows, large_chunk(c.log2n, c.f32)) * (size_t)(c.n / 2) * 2 * es;
+    L.det = 0;
+    L.means = align256(det);
+    L.y = align256(L.means + means);
+    L.total = y ? L.y + y : (means ? L.means + means : det);
+    return L;
+}
+
 int config_set_topk(Config *c, int top_k, double min_period, double max_period);
 
 int make_config(int window_len, int64_t hop, int64_t n_windows, int detrend, int window, int trend_period,
                 int precision, int output, Config *c) {
     const int l = ilog2_exact(window_len);
-    if (l < kMinLog2N || l > kMaxLog2N) {
-        set_error("window_len=%d: must be a power of two in [%d, %d]", window_len, 1 << kMinLog2N, 1 << kMaxLog2N);
+    if (l < kMinLog2N || l > kMaxLog2NLarge) {
+        set_error("window_len=%d: must be a power of two in [%d, %d]", window_len, 1 << kMinLog2N, 1 << kMaxLog2NLarge);
+        return MTB_BAD_ARGS;
+    }
+    if (l > kMaxLog2N && output != MTB_OUT_POWER && output != MTB_OUT_PACKED) {
+        set_error("window_len=%d: windows above %d support the power and packed outputs", window_len, 1 << kMaxLog2N);
         return MTB_BAD_ARGS;
     }
     if (hop < 1 || n_windows < 1) {
@@ -261,6 +286,10 @@ int config_set_topk(Config *c, int top_k, double min_period, double max_period) 
                   min_period, max_period);
         return MTB_BAD_ARGS;
     }
+    if (c->log2n > kMaxLog2N) {
+        set_error("window_len=%d: the top-k scan covers windows up to %d", c->n, 1 << kMaxLog2N);
+        return MTB_BAD_ARGS;
+    }
     if (c->output != MTB_OUT_TOPK_PHASE) c->output = MTB_OUT_TOPK;
     c->topk = top_k;
     c->kmin = (int)ceil((double)c->n / max_period);
@@ -290,6 +319,45 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         I.n_windows = c.n_windows;
         I.log2n = c.log2n;
         HIP_OR(launch_inverse(I, s), MTB_INTERNAL_ERROR);
+        return MTB_OK;
+    }
+    const WsLayout ws = ws_layout(c);
+    char *wsb = static_cast<char *>(d_ws);
+    if (c.log2n > kMaxLog2N) {  // N > 16384: four-step transform (large_fft.hip)
+        LargeLaunch G{};
+        G.series = d_series;
+        G.hop = c.hop;
+        G.detrend = c.detrend;
+        if (c.detrend == MTB_DETREND_KALMAN) {
+            KalmanLaunch K{};
+            K.series = d_series;
+            K.detrended = wsb + ws.det;
+            K.hop = c.hop;
+            K.n_windows = c.n_windows;
+            K.n = c.n;
+            K.f32 = c.f32;
+            memcpy(K.params, kalman, sizeof(K.params));
+            HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
+            G.series = wsb + ws.det;
+            G.hop = c.n;
+            G.detrend = kDetrendNone;
+        } else if (c.detrend == MTB_DETREND_IIR) {
+            const double omega = 2.0 * M_PI / c.trend_period;  // L/WaveSpecZZ_1.0.2.mq5:3041-3043
+            G.iir_alpha = (1.0 - sin(omega)) / cos(omega);
+            G.iir_c = (1.0 - G.iir_alpha) / 2.0;
+        }
+        G.out = d_out;
+        G.twiddle = t.tw;
+        G.detrended = wsb + ws.det;
+        G.means = reinterpret_cast<double *>(wsb + ws.means);
+        G.y = wsb + ws.y;
+        G.n_windows = c.n_windows;
+        G.chunk = large_chunk(c.log2n, c.f32);
+        G.log2n = c.log2n;
+        G.window = c.window;
+        G.packed = c.output == MTB_OUT_PACKED;
+        G.f32 = c.f32;
+        HIP_OR(launch_large(G, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
     SpectrumLaunch L{};
@@ -429,7 +497,7 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
         pc.n_windows = p.nw;
         p.in_bytes = (size_t)pc.series_elems() * es;
         p.out_bytes = (size_t)(p.nw * c.record()) * es;
-        p.ws_bytes = c.detrend == MTB_DETREND_KALMAN ? (size_t)(p.nw * c.n) * es : 0;
+        p.ws_bytes = ws_layout(pc).total;
         p.stream = D.next_stream();
         b->parts.push_back(p);
         Part &P = b->parts.back();
@@ -603,6 +671,10 @@ static int inverse_config(int32_t window_len, int32_t n_windows, Config *c) {
     int st = make_config(window_len, window_len, n_windows, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64,
                          MTB_OUT_PACKED, c);
     c->op = kOpInverse;
+    if (st == MTB_OK && c->log2n > kMaxLog2N) {
+        set_error("window_len=%d: the inverse transform covers windows up to %d", window_len, 1 << kMaxLog2N);
+        return MTB_BAD_ARGS;
+    }
     return st;
 }
 
@@ -877,10 +949,10 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
     }
     Tables t;
     if (get_tables(device, p->cfg.log2n, p->cfg.f32, &t) != MTB_OK) return 0;
-    if (p->cfg.detrend == MTB_DETREND_KALMAN) {
-        p->ws_bytes = (size_t)(p->cfg.n_windows * p->cfg.n) * p->cfg.elem();
+    p->ws_bytes = ws_layout(p->cfg).total;
+    if (p->ws_bytes) {
         if (hipSetDevice(device) != hipSuccess || hipMalloc(&p->d_ws, p->ws_bytes) != hipSuccess) {
-            set_error("hipMalloc(%zu) for the Kalman workspace failed", p->ws_bytes);
+            set_error("hipMalloc(%zu) for the plan workspace failed", p->ws_bytes);
             return 0;
         }
     }

@@ -62,6 +62,27 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream);
 // method 0 unwrapped phase, 1 wrapped phase, 2 group delay; out[n_bins].
 hipError_t launch_phase_row(const double *spec, int n_bins, int method, double *out, hipStream_t stream);
 
+// Windows of N = 32768 .. 262144 (large_fft.hip): four-step transform over
+// a chunk of windows at a time, with the chunk's column results in `y`.
+constexpr int kMaxLog2NLarge = 18;
+struct LargeLaunch {
+    const void *series;   // window w at series + w*hop
+    void *out;            // n_windows records of N/2 (power) or N (packed)
+    const void *twiddle;  // N complex W_N^k, element type
+    void *detrended;      // IIR detrend: n_windows * N elements (else unused)
+    double *means;        // mean detrend: n_windows doubles (else unused)
+    void *y;              // chunk * N/2 complex elements
+    int64_t hop, n_windows, chunk;
+    int log2n, window, detrend;
+    int packed;           // 0 power, 1 packed (Re, Im)
+    bool f32;
+    double iir_alpha, iir_c;
+};
+hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
+// windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
+// profiles/r01/large_chunk_sweep.log; WSP_LARGE_CHUNK_MB overrides)
+int64_t large_chunk(int log2n, bool f32);
+
 // Per-window Kalman 4D detrend pre-pass: d[w*N + j] = x_j - trend_j
 // (one lane per window; trend arithmetic in fp64 like the MQL5 source).
 struct KalmanLaunch {

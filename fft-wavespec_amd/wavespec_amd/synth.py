@@ -52,6 +52,9 @@ CONFIGS = {
                           seed=11, output="topk_phase"),
     "inverse": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="none", seed=11,
                     output="inverse"),
+    # the legacy default InpFFTWindow = 65536 (four-step path), north-star bytes
+    "large": dict(windows=4096, n=65536, hop=65536, precision="f64", detrend="none", window="hann", seed=11),
+    "large_262144": dict(windows=1024, n=262144, hop=262144, precision="f64", detrend="none", window="hann", seed=11),
 }
 
 

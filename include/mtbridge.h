@@ -89,7 +89,8 @@ MTB_API void gpu_shutdown(void);
 /* imports.mqh:7; caller FftProcessor::Run 1.1.0:518-531.  Real forward DFT
  * (unnormalised, e^{-2 pi i k n/N}) of in[0..len) into out[0..len):
  * out[2k] = Re X_k, out[2k+1] = Im X_k for k < len/2.  len: power of two,
- * 32..16384.  Synchronous. */
+ * 32..262144 (the legacy InpFFTWindow menu, L/WaveSpecZZ_1.0.4-new.mq5:657).
+ * Synchronous. */
 MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out);
 
 /* imports.mqh:8-19: MUSIC/ESPRIT cycle extraction lives outside the
@@ -169,7 +170,8 @@ MTB_API int32_t gpu_spectral_phase_unwrap(const double *spectrum, int32_t spectr
  * *out_len = records written.  trend_period: InpTrendPeriod (int > 0) for
  * MTB_DETREND_IIR.  precision: MTB_PREC_F64 or MTB_PREC_F32 (the f32 device
  * path converts the series to float on the host and results back).
- * Synchronous. */
+ * window_len: power of two, 32..262144; above 16384 the outputs are
+ * MTB_OUT_POWER and MTB_OUT_PACKED (four-step transform).  Synchronous. */
 MTB_API int32_t gpu_spectrum_batch(const double *series, int32_t series_len, int32_t window_len, int32_t hop,
                                    int32_t detrend, int32_t window, int32_t trend_period, int32_t precision,
                                    int32_t output, double *out, int32_t out_cap, int32_t *out_len);

@@ -1,0 +1,129 @@
+"""GPU parity of windows above 16384 samples (large_fft.hip: four-step
+transform; SURVEY.md sec. 8f rank 4, the legacy InpFFTWindow menu up to
+262144, L/WaveSpecZZ_1.0.4-new.mq5:657).
+
+Bar as everywhere: per window max_k |P - P_ref| / max_k P_ref <= 1e-10 (fp64)
+against the CPU restatement (whose radix-2 twiddle recurrence is the least
+exact party at these sizes), <= 1e-5 (fp32); numpy.fft as an independent
+exact reference for the fp64 transform itself.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from wavespec_amd import bridge, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"f64": 1e-10, "f32": 1e-5}
+KALMAN = oracle.KALMAN_DEFAULTS
+
+
+def gpu(series, n, hop, detrend="none", window="hann", period=0, prec="f64", output="power"):
+    return bridge.spectrum_batch(series, n, hop, detrend, window, period, prec, output)
+
+
+def ref(series, n, hop, detrend="none", window="hann", period=0, output="power"):
+    return oracle.batch_spectrum(series, n, hop, detrend, window, period, kalman=KALMAN, output=output)
+
+
+def np_power(series, n, hop, window="hann"):
+    nw = 1 + (series.size - n) // hop
+    i = np.arange(n)
+    win = {"none": np.ones(n), "hann": 0.5 * (1 - np.cos(2 * np.pi * i / (n - 1)))}[window]
+    x = np.stack([series[w * hop:w * hop + n] for w in range(nw)]) * win
+    return np.abs(np.fft.fft(x, axis=1)[:, :n // 2]) ** 2
+
+
+@pytest.mark.parametrize("n", [32768, 65536, 131072, 262144])
+def test_large_sizes(gpu_session, n):
+    s = synth.random_walk(3 * n + 17, seed=n % 1000)
+    p = gpu(s, n, n)
+    assert p.shape == (3, n // 2)
+    assert oracle.rel_err(p, ref(s, n, n)) <= TOL["f64"]
+    assert oracle.rel_err(p, np_power(s, n, n)) <= 1e-12
+
+
+@pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024), ("iir", 37), ("kalman", 0)])
+@pytest.mark.parametrize("window", ["none", "hann", "hamming", "blackman", "bartlett"])
+def test_large_detrend_window_matrix(gpu_session, detrend, period, window):
+    n = 65536
+    s = synth.random_walk(2 * n + 5, seed=7)
+    p = gpu(s, n, n, detrend, window, period)
+    assert oracle.rel_err(p, ref(s, n, n, detrend, window, period)) <= TOL["f64"], (detrend, window)
+
+
+@pytest.mark.parametrize("n", [32768, 262144])
+@pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024), ("kalman", 0)])
+def test_large_f32(gpu_session, n, detrend, period):
+    s = synth.random_walk(2 * n, seed=11)
+    p = gpu(s, n, n, detrend, "hann", period, prec="f32")
+    s32 = s.astype(np.float32).astype(np.float64)
+    assert oracle.rel_err(p, ref(s32, n, n, detrend, "hann", period)) <= TOL["f32"]
+
+
+@pytest.mark.parametrize("n", [32768, 131072])
+def test_large_packed(gpu_session, n):
+    s = synth.random_walk(2 * n, seed=3)
+    p = gpu(s, n, n, "none", "hann", output="packed")
+    r = ref(s, n, n, "none", "hann", output="packed")
+    assert p.shape == r.shape == (2, n)
+    assert np.max(np.abs(p - r)) <= 1e-9 * np.max(np.abs(r))
+
+
+@pytest.mark.parametrize("n,hop", [(32768, 1), (32768, 777), (65536, 40001), (131072, 131073)])
+def test_large_hops(gpu_session, n, hop):
+    """Overlapping windows, odd hops (unaligned pair loads), gaps."""
+    s = synth.random_walk(4 * hop + n, seed=hop % 97)
+    p = gpu(s, n, hop, "mean", "hann")
+    assert p.shape[0] == 5
+    assert oracle.rel_err(p, ref(s, n, hop, "mean", "hann")) <= TOL["f64"]
+
+
+def test_large_chunks(gpu_session):
+    """More windows than one chunk of column results (256 at N = 32768 fp64): chunk seams."""
+    n, w = 32768, 300
+    s = synth.random_walk(w * 2048 + n - 2048, seed=5)
+    p = gpu(s, n, 2048, "iir", "hann", 1024)
+    assert p.shape == (w, n // 2)
+    assert oracle.rel_err(p, ref(s, n, 2048, "iir", "hann", 1024)) <= TOL["f64"]
+
+
+def test_large_fft_real_forward(gpu_session):
+    """gpu_fft_real_forward at the legacy default InpFFTWindow = 65536."""
+    n = 65536
+    x = synth.random_walk(n, seed=1)
+    packed = bridge.fft_real_forward(x)
+    re, im = oracle.fft_manual(x)
+    scale = np.max(np.abs(re[:n // 2]))
+    assert np.max(np.abs(packed[0::2] - re[:n // 2])) <= 1e-10 * scale
+    assert np.max(np.abs(packed[1::2] - im[:n // 2])) <= 1e-10 * scale
+
+
+def test_large_rejects_topk_and_inverse(gpu_session):
+    n = 32768
+    s = synth.random_walk(2 * n, seed=2)
+    with pytest.raises(bridge.BridgeError) as e:
+        bridge.spectrum_topk_batch(s, n, n, "none", "hann", top_k=8, min_period=18.0, max_period=200.0)
+    assert e.value.status == -1
+    with pytest.raises(bridge.BridgeError) as e:
+        bridge.fft_real_inverse(np.zeros(n))
+    assert e.value.status == -1
+
+
+def test_large_device_plan(gpu_session):
+    """wsp_plan_* at N = 65536 over 64 windows (chunked column results in the plan workspace)."""
+    import torch
+    n, w = 65536, 64
+    s = synth.random_walk(w * n, seed=9)
+    plan = bridge.Plan(0, n, n, w, "kalman", "hann")
+    try:
+        d_s = torch.from_numpy(s).cuda()
+        d_o = torch.empty(w * (n // 2), dtype=torch.float64, device="cuda")
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        p = d_o.cpu().numpy().reshape(w, n // 2)
+    finally:
+        plan.close()
+    assert oracle.rel_err(p[:8], ref(s[:8 * n], n, n, "kalman", "hann")) <= TOL["f64"]
+    assert oracle.rel_err(p[-4:], ref(s[-4 * n:], n, n, "kalman", "hann")) <= TOL["f64"]
