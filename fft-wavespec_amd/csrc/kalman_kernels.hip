@@ -26,11 +26,11 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
         constexpr size_t kStatic = 4 * 64 * (J + 1) * sizeof(T);
         const size_t reserve = 84 * 1024 - kStatic;  // > half of the CU's 160 KiB: one workgroup per CU
         const unsigned grid = (unsigned)((L.n_windows + 255) / 256);
-        hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 4>), dim3(grid), dim3(256), reserve, stream,
+        hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 4, true>), dim3(grid), dim3(256), reserve, stream,
                            static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp);
     } else {
         const unsigned grid = (unsigned)((L.n_windows + 63) / 64);
-        hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 1>), dim3(grid), dim3(64), 0, stream,
+        hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 1, true>), dim3(grid), dim3(64), 0, stream,
                            static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp);
     }
     return hipGetLastError();

@@ -32,10 +32,10 @@ using namespace wsp;
 static const double kDefaults[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
 
 // launch one variant: WAVES = 4 adds the one-workgroup-per-CU LDS reservation
-template <typename T, int J, int FL, bool TWO, int WAVES>
+template <typename T, int J, int FL, bool TWO, int WAVES, bool PK = false>
 void launch(const T *x, T *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
     const size_t reserve = WAVES == 4 ? 84 * 1024 - 4 * 64 * (J + 1) * sizeof(T) : 0;
-    hipLaunchKernelGGL((kcore::kalman_detrend_kernel<T, T, J, 64, J, FL, TWO, WAVES>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)),
+    hipLaunchKernelGGL((kcore::kalman_detrend_kernel<T, T, J, 64, J, FL, TWO, WAVES, PK>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)),
                        dim3(64 * WAVES), reserve, s, x, d, hop, W, n, kp);
 }
 
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ i
         out[j] = in[j];
 }
 
-template <int FL, bool TWO, int WAVES>
+template <int FL, bool TWO, int WAVES, bool PK = false>
 void time_variant(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n,
                   int reps, hipStream_t s) {
     kcore::KP kp;
@@ -53,9 +53,9 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventCreate(&c));
-    launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+    launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
     CK(hipEventRecord(a, s));
-    for (int r = 0; r < reps; ++r) launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+    for (int r = 0; r < reps; ++r) launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
     CK(hipEventRecord(b, s));
     CK(hipEventSynchronize(b));
     float back, alt = 0;
@@ -63,7 +63,7 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     for (int r = 0; r < reps; ++r) {
         hipLaunchKernelGGL(stream_copy, dim3(8192), dim3(256), 0, s, ci, co, cn);
         CK(hipEventRecord(a, s));
-        launch<float, 32, FL, TWO, WAVES>(x, d, n, W, n, kp, s);
+        launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
         CK(hipEventRecord(c, s));
         CK(hipEventSynchronize(c));
         float t;
@@ -103,6 +103,7 @@ int time_main(int reps) {
         time_variant<3, true, 1>("1-wave WG, static flags, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<3, true, 4>("4-wave WG + 1 WG/CU, static, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<kcore::kKfRuntime, true, 4>("4-wave WG + 1 WG/CU, runtime, two-stage", x, d, ci, co, cn, W, n, reps, s);
+        time_variant<3, true, 4, true>("4-wave WG + 1 WG/CU, static, packed update", x, d, ci, co, cn, W, n, reps, s);
     }
     return 0;
 }
@@ -176,6 +177,30 @@ void check_one(const char *name, const double *dx, double *dd, const std::vector
            (long long)(at % n), (long long)touched);
 }
 
+// fp32 filter (and the packed update) against the same host restatement: relative to the residual scale
+template <bool PK>
+void check_f32(const char *name, const std::vector<double> &x, const std::vector<double> &ref, int64_t W, int64_t hop, int n) {
+    kcore::KP kp;
+    memcpy(&kp, kDefaults, sizeof(kp));
+    std::vector<float> xf(x.begin(), x.end());
+    float *dx, *dd;
+    CK(hipMalloc(&dx, xf.size() * 4));
+    CK(hipMalloc(&dd, W * n * 4));
+    CK(hipMemcpy(dx, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
+    launch<float, 32, 3, true, 4, PK>(dx, dd, hop, W, n, kp, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<float> h(W * n);
+    CK(hipMemcpy(h.data(), dd, W * n * 4, hipMemcpyDeviceToHost));
+    double worst = 0, scale = 0;
+    for (int64_t i = 0; i < W * n; ++i) {
+        worst = fmax(worst, fabs((double)h[i] - ref[i]));
+        scale = fmax(scale, fabs(ref[i]));
+    }
+    printf("%-40s max|d-ref| / max|ref| %.3e\n", name, worst / scale);
+    CK(hipFree(dx));
+    CK(hipFree(dd));
+}
+
 int check_main() {
     const int64_t W = 100, hop = 37;
     const int n = 256;
@@ -201,6 +226,11 @@ int check_main() {
     ema[15] = 12.0;
     for (int64_t w = 0; w < W; ++w) host_kalman(&x[w * hop], n, ema, &ref[w * n]);
     check_one<kcore::kKfRuntime, true, 4>("4-wave runtime two-stage, EMA 12", dx, dd, ref, W, hop, n, ema);
+    std::vector<double> xr(x.size());  // float-rounded prices for the fp32 filters
+    for (size_t i = 0; i < x.size(); ++i) xr[i] = (double)(float)x[i];
+    for (int64_t w = 0; w < W; ++w) host_kalman(&xr[w * hop], n, kDefaults, &ref[w * n]);
+    check_f32<false>("f32 4-wave static two-stage", xr, ref, W, hop, n);
+    check_f32<true>("f32 4-wave static packed update", xr, ref, W, hop, n);
     return 0;
 }
 
