@@ -27,6 +27,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -463,7 +464,51 @@ struct Batch {
     }
 };
 
-// Stages `series` (double, chronological) and enqueues every part.
+// Host-side copies of large batches on several threads (one memcpy thread
+// reaches ~10 GB/s, well below PCIe): f(begin, end) over [0, n) in slices.
+template <typename F> void par_for(int64_t n, int64_t min_per_thread, F f) {
+    const int64_t want = n / std::max<int64_t>(1, min_per_thread);
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(want, 8));
+    if (nt == 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t per = (n + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+        const int64_t b0 = t * per, b1 = std::min<int64_t>(n, b0 + per);
+        if (b0 < b1) th.emplace_back([=] { f(b0, b1); });
+    }
+    f(0, std::min<int64_t>(n, per));
+    for (auto &x : th) x.join();
+}
+void stage_in(void *dst, const double *src, int64_t n, bool f32) {  // series -> pinned staging
+    par_for(n, int64_t(4) << 20, [&](int64_t b0, int64_t b1) {
+        if (f32) {
+            float *d = static_cast<float *>(dst);
+            for (int64_t i = b0; i < b1; ++i) d[i] = (float)src[i];
+        } else {
+            memcpy(static_cast<double *>(dst) + b0, src + b0, (size_t)(b1 - b0) * sizeof(double));
+        }
+    });
+}
+void stage_out(double *dst, const void *src, int64_t n, bool f32) {  // pinned results -> caller
+    par_for(n, int64_t(4) << 20, [&](int64_t b0, int64_t b1) {
+        if (f32) {
+            const float *s = static_cast<const float *>(src);
+            for (int64_t i = b0; i < b1; ++i) dst[i] = (double)s[i];
+        } else {
+            memcpy(dst + b0, static_cast<const double *>(src) + b0, (size_t)(b1 - b0) * sizeof(double));
+        }
+    });
+}
+
+// Stages `series` (double, chronological) and enqueues every part.  A batch
+// is cut into parts: contiguous window ranges per device (the multi-GPU
+// shard), each cut again into up to 16 chunks of >= 64 MiB of input on the
+// device's streams, so that the host staging of chunk i+1, the H2D copy, the
+// kernels and the D2H copy of earlier chunks overlap.  Each part copies its
+// own input slice (with the N - hop halo of overlapping windows).
 int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out) {
     auto b = std::make_unique<Batch>();
     b->cfg = c;
@@ -478,42 +523,47 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
     b->h_in = host_alloc(b->h_in_bytes);
     b->h_out = host_alloc(b->h_out_bytes);
     if (!b->h_in || !b->h_out) return MTB_NO_MEM;
-    if (c.f32) {
-        float *dst = (float *)b->h_in;
-        for (int64_t i = 0; i < in_elems; ++i) dst[i] = (float)series[i];
-    } else {
-        memcpy(b->h_in, series, b->h_in_bytes);
-    }
     const int G = (int)std::min<int64_t>((int64_t)S.devs.size(), c.n_windows);
-    const int64_t per = (c.n_windows + G - 1) / G;
+    const int64_t per_dev = (c.n_windows + G - 1) / G;
+    const int64_t dev_bytes = std::max<int64_t>(1, (per_dev - 1) * c.hop + c.n) * (int64_t)es;
+    const int64_t K = std::max<int64_t>(1, std::min<int64_t>({int64_t(16), dev_bytes / (int64_t(64) << 20), per_dev}));
+    const int64_t per = (per_dev + K - 1) / K;
+    int64_t staged = 0;  // series elements already in the pinned buffer
     for (int g = 0; g < G; ++g) {
-        Part p;
         DeviceCtx &D = *S.devs[g];
-        p.dev = D.dev;
-        p.w0 = g * per;
-        p.nw = std::min<int64_t>(per, c.n_windows - p.w0);
-        if (p.nw <= 0) break;
-        Config pc = c;
-        pc.n_windows = p.nw;
-        p.in_bytes = (size_t)pc.series_elems() * es;
-        p.out_bytes = (size_t)(p.nw * c.record()) * es;
-        p.ws_bytes = ws_layout(pc).total;
-        p.stream = D.next_stream();
-        b->parts.push_back(p);
-        Part &P = b->parts.back();
-        HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
-        P.d_in = dev_alloc(P.dev, P.in_bytes);
-        P.d_out = dev_alloc(P.dev, P.out_bytes);
-        if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
-        if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
-        HIP_OR(hipEventCreateWithFlags(&P.done, hipEventDisableTiming), MTB_INTERNAL_ERROR);
-        const char *src = (const char *)b->h_in + (size_t)(P.w0 * c.hop) * es;
-        HIP_OR(hipMemcpyAsync(P.d_in, src, P.in_bytes, hipMemcpyHostToDevice, P.stream), MTB_INTERNAL_ERROR);
-        int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
-        if (st != MTB_OK) return st;
-        char *dst = (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
-        HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
-        HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+        const int64_t d0 = g * per_dev, d1 = std::min<int64_t>(c.n_windows, d0 + per_dev);
+        for (int64_t w0 = d0; w0 < d1; w0 += per) {
+            Part p;
+            p.dev = D.dev;
+            p.w0 = w0;
+            p.nw = std::min<int64_t>(per, d1 - w0);
+            Config pc = c;
+            pc.n_windows = p.nw;
+            p.in_bytes = (size_t)pc.series_elems() * es;
+            p.out_bytes = (size_t)(p.nw * c.record()) * es;
+            p.ws_bytes = ws_layout(pc).total;
+            p.stream = D.next_stream();
+            b->parts.push_back(p);
+            Part &P = b->parts.back();
+            HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
+            P.d_in = dev_alloc(P.dev, P.in_bytes);
+            P.d_out = dev_alloc(P.dev, P.out_bytes);
+            if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
+            if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
+            HIP_OR(hipEventCreateWithFlags(&P.done, hipEventDisableTiming), MTB_INTERNAL_ERROR);
+            const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
+            if (e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
+                stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
+                staged = e1;
+            }
+            const char *src = (const char *)b->h_in + (size_t)e0 * es;
+            HIP_OR(hipMemcpyAsync(P.d_in, src, P.in_bytes, hipMemcpyHostToDevice, P.stream), MTB_INTERNAL_ERROR);
+            int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
+            if (st != MTB_OK) return st;
+            char *dst = (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
+            HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
+            HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+        }
     }
     *out = std::move(b);
     return MTB_OK;
@@ -521,31 +571,42 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
 
 // MTB_OK when every part finished, MTB_NOT_READY otherwise (non-blocking
 // unless `wait`).
+int part_poll(const Part &p, bool wait) {
+    (void)hipSetDevice(p.dev);
+    hipError_t e = wait ? hipEventSynchronize(p.done) : hipEventQuery(p.done);
+    if (e == hipErrorNotReady) return MTB_NOT_READY;
+    if (e != hipSuccess) {
+        set_error("device %d: %s", p.dev, hipGetErrorString(e));
+        return MTB_INTERNAL_ERROR;
+    }
+    return MTB_OK;
+}
 int batch_poll(Batch &b, bool wait) {
     for (auto &p : b.parts) {
-        (void)hipSetDevice(p.dev);
-        hipError_t e = wait ? hipEventSynchronize(p.done) : hipEventQuery(p.done);
-        if (e == hipErrorNotReady) return MTB_NOT_READY;
-        if (e != hipSuccess) {
-            set_error("device %d: %s", p.dev, hipGetErrorString(e));
-            return MTB_INTERNAL_ERROR;
-        }
+        const int st = part_poll(p, wait);
+        if (st != MTB_OK) return st;
     }
     return MTB_OK;
 }
 
-// Copies finished records (converted to double) into the caller's buffer.
-int32_t batch_copy_out(const Batch &b, double *out, int64_t out_cap) {
+// Copies finished records (converted to double) into the caller's buffer;
+// with `wait`, part by part as each one completes (the copy-out of early
+// parts overlaps the D2H of later ones).
+int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int32_t *n_out) {
     const int64_t rec = b.cfg.record();
     const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
-    const int64_t n = nrec * rec;
-    if (b.cfg.f32) {
-        const float *src = (const float *)b.h_out;
-        for (int64_t i = 0; i < n; ++i) out[i] = (double)src[i];
-    } else {
-        memcpy(out, b.h_out, (size_t)n * sizeof(double));
+    for (const auto &p : b.parts) {
+        if (p.w0 >= nrec) break;
+        if (wait) {
+            const int st = part_poll(p, true);
+            if (st != MTB_OK) return st;
+        }
+        const int64_t r1 = std::min<int64_t>(p.w0 + p.nw, nrec);
+        stage_out(out + p.w0 * rec, (const char *)b.h_out + (size_t)(p.w0 * rec) * b.cfg.elem(), (r1 - p.w0) * rec,
+                  b.cfg.f32);
     }
-    return (int32_t)nrec;
+    *n_out = (int32_t)nrec;
+    return MTB_OK;
 }
 
 int run_sync(const Config &c, const double *series, double *out, int64_t out_cap, int32_t *out_len) {
@@ -557,9 +618,9 @@ int run_sync(const Config &c, const double *series, double *out, int64_t out_cap
     std::unique_ptr<Batch> b;
     int st = batch_start(*S, c, series, &b);
     if (st != MTB_OK) return st;
-    st = batch_poll(*b, true);
+    int32_t n = 0;
+    st = batch_copy_out(*b, out, out_cap, true, &n);
     if (st != MTB_OK) return st;
-    const int32_t n = batch_copy_out(*b, out, out_cap);
     if (out_len) *out_len = n;
     return MTB_OK;
 }
@@ -857,7 +918,9 @@ MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t 
         set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)b.cfg.record());
         return MTB_BAD_ARGS;
     }
-    const int32_t n = batch_copy_out(b, out, out_cap);
+    int32_t n = 0;
+    const int cst = batch_copy_out(b, out, out_cap, false, &n);
+    if (cst != MTB_OK) return cst;
     if (out_len) *out_len = n;
     return MTB_OK;
 }
