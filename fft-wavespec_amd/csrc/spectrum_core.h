@@ -152,12 +152,24 @@ template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int bas
 // Window classes: none; a0 + a1 cos th + a2 cos 2th (Hann, Hamming, Blackman);
 // Bartlett (evaluated exactly as L/WaveSpecZZ_1.0.2.mq5:918-922).
 enum WClass : int { kWinNone = 0, kWinCos = 1, kWinBartlett = 2, kWinCos2 = 3 };  // kWinCos: a2 = 0
-// Ablation bits (tools/kbench.hip only; the library uses 0).
+// Variant bits (tools/kbench.hip ablations; the library's defaults: default_var in spectrum_dispatch.h).
 enum Var : int {
     kVarNoPrefetch = 1, kVarSkeleton = 2, kVarNtLoad = 4, kVarNtStore = 8, kVarBlocked = 16, kVarSkelWide = 32,
     kVarSplitLds = 64,  // real/imaginary halves exchanged separately: half the LDS, 3 waves/SIMD
     kVarOcc4 = 128,     // with kVarSplitLds: 4 waves/SIMD (8 workgroups/CU, <= 128 VGPRs)
     kVarTwTable = 256,  // twiddle powers loaded from the W_N^k table instead of product chains
+    kVarWave1 = 512,    // single-wave workgroups when a window fits one wave (TPW <= 64): no s_barrier
+    kVarDirectStore = 1024,  // power bins stored straight from registers (coalesced 8-B), no LDS staging
+    kVarWinRec = 2048,  // Hann/Hamming values by a 3-term (Chebyshev) recurrence: 3 ops per sample, not 5
+    kVarLdsB64 = 4096,  // with kVarSplitLds: exchange reads as single ds_read_b64 (no ds_read2_b64 pairing)
+};
+
+// Workgroup shape of a variant: kVarWave1 shrinks the workgroup to one wave
+// (64 / TPW windows) when a window needs at most 64 threads.
+template <int LOG2N, int VAR> struct Blk {
+    static constexpr int TPW = Geo<LOG2N>::TPW;
+    static constexpr int BLOCK = ((VAR & kVarWave1) && TPW <= 64) ? 64 : Geo<LOG2N>::BLOCK;
+    static constexpr int WPB = BLOCK / TPW;
 };
 
 template <typename T> struct SpecArgs {
@@ -208,7 +220,7 @@ template <int LOG2N, int PASS> __device__ __forceinline__ int ridx(int t, int i)
 // LDS transpose between passes: write v at widx<PASS>, read v at ridx<PASS+1>.
 // AoS: one complex per ds_write_b128/ds_read_b128 (f64), 2 barriers.  SPLIT:
 // real parts then imaginary parts through half the LDS, 4 barriers.
-template <bool SPLIT, typename T, int LOG2N, int PASS>
+template <int SPLIT, typename T, int LOG2N, int PASS>
 __device__ __forceinline__ void exchange(char *base, cpx<T> (&v)[16], int t) {
     if constexpr (!SPLIT) {
         cpx<T> *s = reinterpret_cast<cpx<T> *>(base);
@@ -219,19 +231,25 @@ __device__ __forceinline__ void exchange(char *base, cpx<T> (&v)[16], int t) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = s[ridx<LOG2N, PASS + 1>(t, i)];
     } else {
+        // SPLIT == 2: the reads go through a volatile view so that the compiler keeps them as
+        // single ds_read_b64 (2 LDS cycles each) instead of pairing them into ds_read2_b64
+        // (8 cycles for the same 16 bytes, MI355X_MICROARCH.md LDS table)
         T *s = reinterpret_cast<T *>(base);
+        using RT = std::conditional_t<SPLIT == 2, const volatile __attribute__((address_space(3))) T,
+                                      const __attribute__((address_space(3))) T>;
+        RT *rs = (RT *)s;  // LDS address space: the volatile view must stay a ds_read, not a flat load
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].re;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i].re = s[ridx<LOG2N, PASS + 1>(t, i)];
+        for (int i = 0; i < 16; ++i) v[i].re = rs[ridx<LOG2N, PASS + 1>(t, i)];
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].im;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i].im = s[ridx<LOG2N, PASS + 1>(t, i)];
+        for (int i = 0; i < 16; ++i) v[i].im = rs[ridx<LOG2N, PASS + 1>(t, i)];
     }
 }
 
@@ -255,16 +273,30 @@ __device__ __forceinline__ void twiddle(cpx<T> *v, const cpx<T> *__restrict__ tw
     }
 }
 
-template <bool SPLIT, bool TABLE, typename T, int LOG2N, int PASS>
+template <int SPLIT, bool TABLE, typename T, int LOG2N, int PASS>
 __device__ __forceinline__ void mid_passes(char *base, cpx<T> (&v)[16], const cpx<T> *__restrict__ tw, int t) {
     using G = Geo<LOG2N>;
     if constexpr (PASS < G::NPASS - 1) {
         constexpr int R = G::radix(PASS), Ns = G::ns(PASS), BPT = 16 / R;
+        if constexpr (!TABLE && BPT > 1 && G::TPW % Ns == 0) {
+            // every group q has b % Ns = t % Ns: one product chain of W^(r k1) serves all of them
+            const cpx<T> w = tw[(t % Ns) * (G::N / (Ns * R))];
+            cpx<T> wr = w;
 #pragma unroll
-        for (int q = 0; q < BPT; ++q) {
-            const int b = t + G::TPW * q;
-            twiddle<TABLE, T, R>(&v[q * R], tw, (b % Ns) * (G::N / (Ns * R)));
-            dft<T, R>(&v[q * R]);
+            for (int r = 1; r < R; ++r) {
+#pragma unroll
+                for (int q = 0; q < BPT; ++q) v[q * R + r] = cmul(v[q * R + r], wr);
+                if (r + 1 < R) wr = cmul(wr, w);
+            }
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) dft<T, R>(&v[q * R]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const int b = t + G::TPW * q;
+                twiddle<TABLE, T, R>(&v[q * R], tw, (b % Ns) * (G::N / (Ns * R)));
+                dft<T, R>(&v[q * R]);
+            }
         }
         exchange<SPLIT, T, LOG2N, PASS>(base, v, t);
         mid_passes<SPLIT, TABLE, T, LOG2N, PASS + 1>(base, v, tw, t);
@@ -501,7 +533,7 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
                                            typename V2<T>::t (&raw)[16]) {
     using G = Geo<LOG2N>;
     using v2 = typename V2<T>::t;
-    const int64_t w = g * G::WPB + slot;
+    const int64_t w = g * Blk<LOG2N, VAR>::WPB + slot;
     const T *__restrict__ xw = a.series + (w < a.n_windows ? w : 0) * a.hop;
     if (a.vec) {
 #pragma unroll
@@ -526,13 +558,13 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
-__global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
+__global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
     using G = Geo<LOG2N>;
     using v2 = typename V2<T>::t;
-    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B, NWV = G::NWV;
+    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = Blk<LOG2N, VAR>::WPB, SLOT = G::SLOT, B = G::B, NWV = G::NWV;
     constexpr int R0 = G::R0, BPT0 = G::BPT0;
     constexpr bool kPrefetch = !(VAR & kVarNoPrefetch);
-    constexpr bool kSplit = VAR & kVarSplitLds;
+    constexpr int kSplit = (VAR & kVarSplitLds) ? ((VAR & kVarLdsB64) ? 2 : 1) : 0;
     constexpr int kCplx = WPB * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));
     constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
     constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
@@ -677,6 +709,31 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & k
 
         // ---- window (fp64) + pass 0 (no twiddles: Ns = 1)
         cpx<T> v[16];
+        constexpr bool kRec = (VAR & kVarWinRec) && WCLASS == kWinCos && R0 >= 8;
+        if constexpr (kRec) {
+            // h(i) = a0 + a1 cos(th i) along the thread's even samples i = i0 + D r (D = 2M/R0) and
+            // odd samples i0 + 1 + D r: h_(r+1) = 2C h_r - h_(r-1) + a0 (2 - 2C), C = cos(th D) = a.cs.
+            // Seeds h_0, h_1 of both sequences from the per-thread rotation start; the recurrence
+            // amplifies rounding by at most 1/sin(th D) (~2.6 at R0 = 16) over <= 15 steps.
+            const double C2 = 2.0 * a.cs, K = a.a0 * (2.0 - C2);
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q) {
+                double c = wc0[q], s = ws0[q];
+                asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no hoisted seeds
+                const double c1 = c * a.cs - s * a.ss, s1 = s * a.cs + c * a.ss;
+                double he0 = a.a0 + a.a1 * c, he1 = a.a0 + a.a1 * c1;
+                double ho0 = a.a0 + a.a1 * (c * a.co - s * a.so), ho1 = a.a0 + a.a1 * (c1 * a.co - s1 * a.so);
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    v[q * R0 + r] = {T(xa[q * R0 + r] * he0), T(xb[q * R0 + r] * ho0)};
+                    const double he2 = fma(C2, he1, K - he0), ho2 = fma(C2, ho1, K - ho0);
+                    he0 = he1;
+                    he1 = he2;
+                    ho0 = ho1;
+                    ho1 = ho2;
+                }
+            }
+        } else {
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) {
             double c = 0.0, s = 0.0;
@@ -710,6 +767,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & k
                 v[q * R0 + r] = {T(da), T(db)};
             }
         }
+        }  // !kRec
 
         if constexpr (VAR & kVarSkelWide) {
             // memory-pattern ablation with 16-B contiguous stores
@@ -786,7 +844,8 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & k
         const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
         T *prow = reinterpret_cast<T *>(lbase);  // power row staged in this window's LDS slot
-        if constexpr (OUT != kOutPacked) __syncthreads();  // every final-pass LDS read is done
+        constexpr bool kDirect = OUT == kOutPower && (VAR & kVarDirectStore);
+        if constexpr (OUT != kOutPacked && !kDirect) __syncthreads();  // every final-pass LDS read is done
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const cpx<T> A = u0[s], Bv = u1[7 - s];
@@ -805,7 +864,19 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & k
                     xb = {T(2) * Bv.re, T(-2) * Bv.im};
                 }
             }
-            if constexpr (OUT == kOutPower) {
+            if constexpr (kDirect) {  // lanes t, t+1 -> bins ka, ka+1 (kb, kb-1): 512-B runs per wave store
+                if (active) {
+                    const T pa = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
+                    const T pb = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+                    if constexpr (VAR & kVarNtStore) {
+                        __builtin_nontemporal_store(pa, a.out + w * M + ka);
+                        __builtin_nontemporal_store(pb, a.out + w * M + kb);
+                    } else {
+                        a.out[w * M + ka] = pa;
+                        a.out[w * M + kb] = pb;
+                    }
+                }
+            } else if constexpr (OUT == kOutPower) {
                 prow[ka] = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
                 prow[kb] = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
             } else if constexpr (OUT == kOutTopK || kPhase) {  // stage X for the scan (AoS slot)
@@ -969,7 +1040,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, (VAR & kVarSplitLds) ? ((VAR & k
                 }
             }
         }
-        if constexpr (OUT == kOutPower) {
+        if constexpr (OUT == kOutPower && !kDirect) {
             // write the row back with contiguous 16-B stores (1 KiB per wave instruction)
             constexpr int VE = 16 / (int)sizeof(T);
             typedef T vst __attribute__((ext_vector_type(16 / sizeof(T))));

@@ -64,20 +64,27 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
 // do not overlap (a.nt).  The IIR path (33 KiB detrend staging caps it at 4
 // workgroups/CU anyway) and the packed output (spills at 168 VGPRs) keep the
 // AoS exchange at 2 waves/SIMD.
-constexpr int kDefaultVar = kVarNoPrefetch | kVarNtStore | kVarSplitLds;
+// Round-1 additions on every path (profiles/r01/kbench_hop1_n*.log, kbench_ns_b64.log): single-wave
+// workgroups when a window fits one wave (no cross-wave s_barrier), Hann/Hamming by the 3-term
+// recurrence, and -- split exchange -- single ds_read_b64 reads instead of the compiler's
+// ds_read2_b64 pairs: hop = 1 at N = 512/1024/2048/4096 -7/-8/-7/-3 %, north star -2.5 %.
+constexpr int kCommonVar = kVarNoPrefetch | kVarNtStore | kVarWave1 | kVarWinRec;
+constexpr int kDefaultVar = kCommonVar | kVarSplitLds | kVarLdsB64;
 constexpr int kDefaultGrid = 32768;
 template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var() {
     // the f32 mean path converts every sample to fp64 for the reduction and spills at 168;
     // N > 4096 runs one 256/512-thread workgroup per window, where the split exchange cannot
     // raise occupancy (LDS and VGPRs allow 2 waves/SIMD either way)
-    return (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
-               ? (kVarNoPrefetch | kVarNtStore)
+    // (the phase outputs keep the round-1 starting point: their register budget is the tightest)
+    return (OUT == kOutPhase || OUT == kOutTopKPhase) ? (kVarNoPrefetch | kVarNtStore)
+           : (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
+               ? kCommonVar
                : kDefaultVar;
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
 hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
-    using G = Geo<LOG2N>;
+    using G = Blk<LOG2N, VAR>;
     const SpecArgs<T> a = make_args<T>(L, G::WPB);
     int64_t grid = L.grid > 0 ? L.grid : kDefaultGrid;
     if (grid > a.n_groups) grid = a.n_groups;

@@ -6,6 +6,7 @@
 //   kbench [log2n=12] [windows=65536] [reps=20] [rounds=3]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -160,49 +161,102 @@ int out_main(int reps) {
     return 0;
 }
 
-template <int VAR>
-float time_c4(const SpectrumLaunch &L, int reps) {
+template <int LOG2N, int VAR>
+float time_h1(const SpectrumLaunch &L, int reps) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    CK((launch_one<double, 11, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) CK((launch_one<double, 11, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    for (int i = 0; i < reps; ++i) CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
     return ms * 1000.f / reps;
 }
 
-// C4 shape: 1M windows x 2048, hop = 1 (compute-bound)
-int c4_main(int reps) {
-    const int64_t W = 1 << 20;
-    const int n = 2048;
+// per-window max |P - P_ref| / max P_ref of one launch of a variant against `ref`
+template <int LOG2N, int VAR>
+double check_h1(const SpectrumLaunch &L, const std::vector<double> &ref) {
+    std::vector<double> got(ref.size());
+    CK(hipMemset(L.out, 0, got.size() * 8));
+    CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK(hipMemcpy(got.data(), L.out, got.size() * 8, hipMemcpyDeviceToHost));
+    const size_t m = size_t(1) << (LOG2N - 1);
+    double worst = 0;
+    for (size_t w = 0; w * m < ref.size(); ++w) {
+        double mx = 0, d = 0;
+        for (size_t k = 0; k < m; ++k) {
+            mx = std::max(mx, std::fabs(ref[w * m + k]));
+            d = std::max(d, std::fabs(got[w * m + k] - ref[w * m + k]));
+        }
+        worst = std::max(worst, mx > 0 ? d / mx : d);
+    }
+    return worst;
+}
+
+template <int LOG2N> struct H1Var {
+    const char *name;
+    float (*time)(const SpectrumLaunch &, int);
+    double (*check)(const SpectrumLaunch &, const std::vector<double> &);
+};
+#define H1V(NAME, V) H1Var<LOG2N>{NAME, &time_h1<LOG2N, (V)>, &check_h1<LOG2N, (V)>}
+
+// hop = 1 shapes (C4: 1M windows x 2048; the C5 lengths): VALU/LDS-bound, so the
+// variants trade instructions, barriers and LDS round trips
+template <int LOG2N>
+int hop1_main(int64_t W, int reps) {
+    const int n = 1 << LOG2N;
     double *x, *out, *tw;
     CK(hipMalloc(&x, (W + n) * 8));
-    CK(hipMalloc(&out, W * n / 2 * 8));
+    CK(hipMalloc(&out, W * (n / 2) * 8));
     CK(hipMalloc(&tw, n * 16));
     std::vector<double> h(2 * n);
     for (int k = 0; k < n; ++k) {
-        long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
-        h[2 * k] = (double)cosl(a);
-        h[2 * k + 1] = (double)sinl(a);
+        long double ang = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+        h[2 * k] = (double)cosl(ang);
+        h[2 * k + 1] = (double)sinl(ang);
     }
     CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(fill_walk, dim3(1024), dim3(256), 0, 0, x, W + n);
     CK(hipDeviceSynchronize());
     SpectrumLaunch L{};
-    L.series = x; L.out = out; L.twiddle = tw; L.window = 1; L.hop = 1; L.n_windows = W; L.log2n = 11;
+    L.series = x; L.out = out; L.twiddle = tw; L.window = 1; L.hop = 1; L.n_windows = W; L.log2n = LOG2N;
     const double bytes = (W + n) * 8.0 + W * (n / 2) * 8.0;
+    printf("# hop=1 W=%lld N=%d algorithmic bytes=%.3f GB, roofline %.1f us\n", (long long)W, n, bytes / 1e9,
+           bytes / 8e6);
+    constexpr int S = kVarSplitLds | kVarNoPrefetch | kVarNtStore, A = kVarNoPrefetch | kVarNtStore;
+    const H1Var<LOG2N> vars[] = {
+        H1V("split", S),
+        H1V("split+w1", S | kVarWave1),
+        H1V("split+direct", S | kVarDirectStore),
+        H1V("split+rec", S | kVarWinRec),
+        H1V("split+b64", S | kVarLdsB64),
+        H1V("split+w1+rec", S | kVarWave1 | kVarWinRec),
+        H1V("split+w1+rec+b64", S | kVarWave1 | kVarWinRec | kVarLdsB64),
+        H1V("split+rec+b64", S | kVarWinRec | kVarLdsB64),
+        H1V("aos+w1+rec", A | kVarWave1 | kVarWinRec),
+    };
+    {  // every variant against the previous library default on the first 4096 windows
+        std::vector<double> ref((size_t)4096 * (n / 2));
+        SpectrumLaunch R = L;
+        R.n_windows = 4096;
+        CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, S>(R, 0)));
+        CK(hipMemcpy(ref.data(), out, ref.size() * 8, hipMemcpyDeviceToHost));
+        for (const auto &v : vars) printf("check %-28s max rel err vs split %.3e\n", v.name, v.check(R, ref));
+        fflush(stdout);
+    }
     for (int round = 0; round < 2; ++round)
-        for (int g : {16384, 32768, 65536}) {
+        for (int g : {32768, 65536, 131072}) {
             L.grid = g;
-            const float a = time_c4<kVarSplitLds | kVarNoPrefetch | kVarNtStore>(L, reps);
-            const float b = time_c4<kVarSplitLds | kVarNoPrefetch | kVarNtStore | kVarTwTable>(L, reps);
-            const float c = time_c4<kVarNoPrefetch | kVarNtStore>(L, reps);
-            printf("round %d c4 grid=%6d  split %8.1f us (%6.1f GB/s)  split+twtab %8.1f us  aos %8.1f us\n", round, g, a,
-                   bytes / a / 1e3, b, c);
+            for (const auto &v : vars) {
+                const float us = v.time(L, reps);
+                printf("round %d grid=%6d %-28s %8.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", round, g, v.name, us,
+                       bytes / us / 1e3, bytes / us / 1e3 / 8000.0);
+            }
             fflush(stdout);
         }
     return 0;
@@ -210,7 +264,18 @@ int c4_main(int reps) {
 
 
 int main(int argc, char **argv) {
-    if (argc > 1 && std::string(argv[1]) == "c4") return c4_main(argc > 2 ? atoi(argv[2]) : 5);
+    if (argc > 1 && std::string(argv[1]) == "hop1") {  // kbench hop1 [log2n=11] [windows=1M] [reps=5]
+        const int lg = argc > 2 ? atoi(argv[2]) : 11;
+        const int64_t W = argc > 3 ? atoll(argv[3]) : (1 << 20);
+        const int reps = argc > 4 ? atoi(argv[4]) : 5;
+        switch (lg) {
+        case 9: return hop1_main<9>(W, reps);
+        case 10: return hop1_main<10>(W, reps);
+        case 11: return hop1_main<11>(W, reps);
+        case 12: return hop1_main<12>(W, reps);
+        default: return 1;
+        }
+    }
     if (argc > 1 && std::string(argv[1]) == "out") return out_main(argc > 2 ? atoi(argv[2]) : 20);
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -286,7 +351,9 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[3] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+            } r[4] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+                      {"split+nt2+rec+b64", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore |
+                                                         kVarWinRec | kVarLdsB64>(L, s, reps)},
                       {"split+nt2+twtab", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore | kVarTwTable>(L, s, reps)},
                       {"skelwide", time_variant<kVarSkelWide | kVarNoPrefetch | kVarNtLoad>(L, s, reps)}};
             for (auto &v : r)
