@@ -11,7 +11,7 @@ TAG=$1; CFG=${2:-north_star}
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline > $OUT/trace.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 100 --warmup 20 --no-cpu-baseline > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
   python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
