@@ -101,15 +101,35 @@ def timed_steps(step, sync, ctl: Control, steps: int, warmup: int) -> float:
     return ctl.max(t1 - t0)
 
 
-def cpu_baseline(d_series, cfg: dict, budget_s: float) -> dict:
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_threads() -> int:
+    """Threads for the all-core leg: the job's CPU share (OMP_NUM_THREADS on the GPU box), at most 16."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(16, n or (os.cpu_count() or 1)))
+
+
+def cpu_baseline(d_series, cfg: dict, budget_s: float, threads: int = 1) -> dict:
     """Oracle (CPU restatement of the reference per-window path, C -O3) on
-    1 core, on the leading windows of the same device-resident workload
+    `threads` cores (OpenMP over windows; 1 = the single-threaded MQL5
+    OnCalculate), on the leading windows of the same device-resident workload
     (copied to the host chunk by chunk, outside the timed CPU work), for
     about budget_s seconds."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
     lib = oracle.lib()
-    lib.ora_set_threads(1)
+    threads = lib.ora_set_threads(threads)
     n, hop = cfg["n"], cfg["hop"]
     out = cfg.get("output", "power")
     args = (n, hop, cfg["detrend"], cfg["window"], cfg.get("trend_period", 0))
@@ -126,7 +146,7 @@ def cpu_baseline(d_series, cfg: dict, budget_s: float) -> dict:
         else:
             oracle.batch_spectrum(seg, *args, kalman=oracle.KALMAN_DEFAULTS)
 
-    chunk = 256
+    chunk = 256 * threads
     done, spent = 0, 0.0
     max_w = cfg["windows"]
     while spent < budget_s and done < max_w:
@@ -137,10 +157,11 @@ def cpu_baseline(d_series, cfg: dict, budget_s: float) -> dict:
         spent += time.perf_counter() - t0
         done += take
     dt = spent
-    return {"value": done / dt, "unit": "windows/s", "cores": 1, "kind": "port",
+    lib.ora_set_threads(1)
+    return {"value": done / dt, "unit": "windows/s", "cores": threads, "kind": "port",
             "sample": f"first {done} windows of the same {cfg['windows']}x{n} workload (hop={hop}, "
                       f"{cfg['detrend']} detrend, {cfg['window']} window, output {out}), "
-                      f"oracle/wavespec_oracle.c -O3, 1 thread, {dt:.1f} s"}
+                      f"oracle/wavespec_oracle.c -O3, {threads} thread(s) on {cpu_model()}, {dt:.1f} s"}
 
 
 def load_traffic(config: str):
@@ -194,11 +215,12 @@ def run_c5(args, rank, local_rank, world, ctl):
     ev1.synchronize()
     step_s = ev0.elapsed_time(ev1) / 1e3 / reps
     value = ctl.sum(float(total_w * args.steps)) / secs
-    baseline = None
+    baseline = baseline_all = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         plan0, s0, _, _ = jobs[-1]  # a 4096-pt symbol: the costliest per window
-        baseline = cpu_baseline(s0, {"n": 4096, "hop": 1, "windows": plan0.n_windows, "detrend": "none",
-                                     "window": "hann"}, args.cpu_seconds)
+        c5cfg = {"n": 4096, "hop": 1, "windows": plan0.n_windows, "detrend": "none", "window": "hann"}
+        baseline = cpu_baseline(s0, c5cfg, args.cpu_seconds)
+        baseline_all = cpu_baseline(s0, c5cfg, args.cpu_seconds / 2, cpu_threads())
     if rank == 0:
         achieved = alg / step_s / 1e9
         per_launch = load_traffic("c5")  # PMC bytes per spectrum dispatch; one step is len(jobs) dispatches
@@ -215,7 +237,7 @@ def run_c5(args, rank, local_rank, world, ctl):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": c5_traffic,
                          "algorithmic_bytes_per_launch": alg, "kernel_ms": step_s * 1e3,
                          "note": "one step = 28 launches on 4 streams; time per step from HIP events"},
-            "cpu_baseline": baseline}), flush=True)
+            "cpu_baseline": baseline, "cpu_baseline_all_cores": baseline_all}), flush=True)
     for j in jobs:
         j[0].close()
     ctl.close()
@@ -275,9 +297,10 @@ def main():
 
     total_windows = ctl.sum(float(w * args.steps))
     value = total_windows / secs
-    baseline = None
+    baseline = baseline_all = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         baseline = cpu_baseline(d_series, cfg, args.cpu_seconds)
+        baseline_all = cpu_baseline(d_series, cfg, args.cpu_seconds / 2, cpu_threads())
 
     if rank == 0:
         traffic = load_traffic(args.config)
@@ -305,6 +328,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_s * 1e3},
             "cpu_baseline": baseline,
+            "cpu_baseline_all_cores": baseline_all,
         }
         print(json.dumps(line), flush=True)
     plan.close()
