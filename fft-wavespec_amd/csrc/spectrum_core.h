@@ -840,6 +840,9 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         // ---- real-to-complex post-processing + |X|^2, one slot per (k, M-k):
         // E = (Z[k] + conj Z[M-k])/2, O = -i (Z[k] - conj Z[M-k])/2,
         // X[k] = E + W_N^k O, X[M-k] = conj(E - W_N^k O).
+        // the 1/2 of E, O (and 1/4 of |X|^2): folded into the window coefficients for the cosine
+        // windows (make_args halves a0, a1, a2 -- an exact power-of-two scaling, bit-identical results)
+        constexpr T kS1 = kCosWin ? T(1) : T(0.5), kS2 = kCosWin ? T(1) : T(0.25);
         const cpx<T> wt = a.tw[t];
         const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
@@ -866,8 +869,8 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             }
             if constexpr (kDirect) {  // lanes t, t+1 -> bins ka, ka+1 (kb, kb-1): 512-B runs per wave store
                 if (active) {
-                    const T pa = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
-                    const T pb = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+                    const T pa = kS2 * (xa.re * xa.re + xa.im * xa.im);
+                    const T pb = kS2 * (xb.re * xb.re + xb.im * xb.im);
                     if constexpr (VAR & kVarNtStore) {
                         __builtin_nontemporal_store(pa, a.out + w * M + ka);
                         __builtin_nontemporal_store(pb, a.out + w * M + kb);
@@ -877,18 +880,18 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                     }
                 }
             } else if constexpr (OUT == kOutPower) {
-                prow[ka] = T(0.25) * (xa.re * xa.re + xa.im * xa.im);
-                prow[kb] = T(0.25) * (xb.re * xb.re + xb.im * xb.im);
+                prow[ka] = kS2 * (xa.re * xa.re + xa.im * xa.im);
+                prow[kb] = kS2 * (xb.re * xb.re + xb.im * xb.im);
             } else if constexpr (OUT == kOutTopK || kPhase) {  // stage X for the scan (AoS slot)
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
-                xrow[kPhase ? pad16(ka) : ka] = {T(0.5) * xa.re, T(0.5) * xa.im};
-                xrow[kPhase ? pad16(kb) : kb] = {T(0.5) * xb.re, T(0.5) * xb.im};
+                xrow[kPhase ? pad16(ka) : ka] = {kS1 * xa.re, kS1 * xa.im};
+                xrow[kPhase ? pad16(kb) : kb] = {kS1 * xb.re, kS1 * xb.im};
             } else if (active) {  // packed: (Re, Im) of one bin is already one 16-B (8-B) store
                 v2 oa, ob;
-                oa.x = T(0.5) * xa.re;
-                oa.y = T(0.5) * xa.im;
-                ob.x = T(0.5) * xb.re;
-                ob.y = T(0.5) * xb.im;
+                oa.x = kS1 * xa.re;
+                oa.y = kS1 * xa.im;
+                ob.x = kS1 * xb.re;
+                ob.y = kS1 * xb.im;
                 *reinterpret_cast<v2 *>(a.out + w * N + 2 * ka) = oa;
                 *reinterpret_cast<v2 *>(a.out + w * N + 2 * kb) = ob;
             }

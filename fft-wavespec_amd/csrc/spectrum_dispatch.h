@@ -34,7 +34,13 @@ template <typename T> SpecArgs<T> make_args(const SpectrumLaunch &L, int wpb) {
     a.vec = L.vec_mode == 1 ? 0 : L.vec_mode == 2 ? 1 : ((L.hop % 2 == 0) && (reinterpret_cast<uintptr_t>(L.series) % (2 * sizeof(T)) == 0));
     // overlapping windows re-read samples from L2/MALL: keep them cacheable
     a.nt = L.nt_mode == 2 || (L.nt_mode == 0 && L.hop >= (int64_t(1) << L.log2n));
-    window_class(L.window, &a.a0, &a.a1, &a.a2);
+    const int wclass = window_class(L.window, &a.a0, &a.a1, &a.a2);
+    if (wclass == kWinCos || wclass == kWinCos2) {
+        // cosine windows carry the R2C step's factor 1/2 (spectrum_kernel: kS1, kS2)
+        a.a0 *= 0.5;
+        a.a1 *= 0.5;
+        a.a2 *= 0.5;
+    }
     const int n = 1 << L.log2n;
     const int m = n / 2;
     const int log2m = L.log2n - 1;
