@@ -239,6 +239,8 @@ int hop1_main(int64_t W, int reps) {
         H1V("split+w1+rec+b64", S | kVarWave1 | kVarWinRec | kVarLdsB64),
         H1V("split+rec+b64", S | kVarWinRec | kVarLdsB64),
         H1V("aos+w1+rec", A | kVarWave1 | kVarWinRec),
+        H1V("split+w1+rec+b64+occ4", S | kVarWave1 | kVarWinRec | kVarLdsB64 | kVarOcc4),
+        H1V("split+w1+rec+b64+prefetch", (S & ~kVarNoPrefetch) | kVarWave1 | kVarWinRec | kVarLdsB64),
     };
     {  // every variant against the previous library default on the first 4096 windows
         std::vector<double> ref((size_t)4096 * (n / 2));
