@@ -162,6 +162,7 @@ enum Var : int {
     kVarDirectStore = 1024,  // power bins stored straight from registers (coalesced 8-B), no LDS staging
     kVarWinRec = 2048,  // Hann/Hamming values by a 3-term (Chebyshev) recurrence: 3 ops per sample, not 5
     kVarLdsB64 = 4096,  // with kVarSplitLds: exchange reads as single ds_read_b64 (no ds_read2_b64 pairing)
+    kVarWinTab = 8192,  // window values (with the R2C factor 1/2) from an fp64 table a.win (L1/L2-resident)
 };
 
 // Workgroup shape of a variant: kVarWave1 shrinks the workgroup to one wave
@@ -183,6 +184,7 @@ template <typename T> struct SpecArgs {
     // by (co, so) from an even to the next odd sample
     double a0, a1, a2, cs, ss, co, so, inv_theta;  // inv_theta = 2 pi/(N-1)
     double inv_nm1;                  // 1/(N-1) for Bartlett
+    const double *__restrict__ win;  // kVarWinTab: h(i)/2, i < N (cosine windows)
     int topk, kmin, kmax;            // kOutTopK(Phase): k slots over bins [kmin, kmax]
     double alpha, c;                 // IIR trend (L/WaveSpecZZ_1.0.2.mq5:3041-3043)
     double apow[8];                  // alpha^(32 * 2^j)
@@ -710,7 +712,15 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         // ---- window (fp64) + pass 0 (no twiddles: Ns = 1)
         cpx<T> v[16];
         constexpr bool kRec = (VAR & kVarWinRec) && WCLASS == kWinCos && R0 >= 8;
-        if constexpr (kRec) {
+        if constexpr ((VAR & kVarWinTab) && kCosWin) {
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const d2v h = *reinterpret_cast<const d2v *>(a.win + 2 * ((t + TPW * q) + (M / R0) * r));
+                    v[q * R0 + r] = {T(xa[q * R0 + r] * h.x), T(xb[q * R0 + r] * h.y)};
+                }
+        } else if constexpr (kRec) {
             // h(i) = a0 + a1 cos(th i) along the thread's even samples i = i0 + D r (D = 2M/R0) and
             // odd samples i0 + 1 + D r: h_(r+1) = 2C h_r - h_(r-1) + a0 (2 - 2C), C = cos(th D) = a.cs.
             // Seeds h_0, h_1 of both sequences from the per-thread rotation start; the recurrence

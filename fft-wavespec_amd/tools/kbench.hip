@@ -161,14 +161,32 @@ int out_main(int reps) {
     return 0;
 }
 
+static const double *g_win = nullptr;  // window table of the hop1 mode (kVarWinTab variants)
+
+// launch_one with the window table patched into the arguments
+template <int LOG2N, int VAR> hipError_t launch_h1(const SpectrumLaunch &L, hipStream_t s) {
+    if constexpr (!(VAR & kVarWinTab)) {
+        return launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, s);
+    } else {
+        using G = Blk<LOG2N, VAR>;
+        SpecArgs<double> a = make_args<double>(L, G::WPB);
+        a.win = g_win;
+        int64_t grid = L.grid > 0 ? L.grid : kDefaultGrid;
+        if (grid > a.n_groups) grid = a.n_groups;
+        hipLaunchKernelGGL((spectrum_kernel<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>), dim3((unsigned)grid),
+                           dim3(G::BLOCK), 0, s, a);
+        return hipGetLastError();
+    }
+}
+
 template <int LOG2N, int VAR>
 float time_h1(const SpectrumLaunch &L, int reps) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK((launch_h1<LOG2N, VAR>(L, 0)));
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    for (int i = 0; i < reps; ++i) CK((launch_h1<LOG2N, VAR>(L, 0)));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -183,7 +201,7 @@ template <int LOG2N, int VAR>
 double check_h1(const SpectrumLaunch &L, const std::vector<double> &ref) {
     std::vector<double> got(ref.size());
     CK(hipMemset(L.out, 0, got.size() * 8));
-    CK((launch_one<double, LOG2N, kDetrendNone, kOutPower, kWinCos, VAR>(L, 0)));
+    CK((launch_h1<LOG2N, VAR>(L, 0)));
     CK(hipMemcpy(got.data(), L.out, got.size() * 8, hipMemcpyDeviceToHost));
     const size_t m = size_t(1) << (LOG2N - 1);
     double worst = 0;
@@ -223,6 +241,13 @@ int hop1_main(int64_t W, int reps) {
     CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(fill_walk, dim3(1024), dim3(256), 0, 0, x, W + n);
     CK(hipDeviceSynchronize());
+    std::vector<double> hw(n);  // Hann/2 (the R2C factor folded in, as make_args does for the coefficients)
+    for (int i = 0; i < n; ++i)
+        hw[i] = (double)(0.25L - 0.25L * cosl(6.283185307179586476925286766559005768L * i / (long double)(n - 1)));
+    double *win;
+    CK(hipMalloc(&win, n * 8));
+    CK(hipMemcpy(win, hw.data(), n * 8, hipMemcpyHostToDevice));
+    g_win = win;
     SpectrumLaunch L{};
     L.series = x; L.out = out; L.twiddle = tw; L.window = 1; L.hop = 1; L.n_windows = W; L.log2n = LOG2N;
     const double bytes = (W + n) * 8.0 + W * (n / 2) * 8.0;
@@ -239,8 +264,7 @@ int hop1_main(int64_t W, int reps) {
         H1V("split+w1+rec+b64", S | kVarWave1 | kVarWinRec | kVarLdsB64),
         H1V("split+rec+b64", S | kVarWinRec | kVarLdsB64),
         H1V("aos+w1+rec", A | kVarWave1 | kVarWinRec),
-        H1V("split+w1+rec+b64+occ4", S | kVarWave1 | kVarWinRec | kVarLdsB64 | kVarOcc4),
-        H1V("split+w1+rec+b64+prefetch", (S & ~kVarNoPrefetch) | kVarWave1 | kVarWinRec | kVarLdsB64),
+        H1V("split+w1+tab+b64", S | kVarWave1 | kVarWinTab | kVarLdsB64),
     };
     {  // every variant against the previous library default on the first 4096 windows
         std::vector<double> ref((size_t)4096 * (n / 2));
