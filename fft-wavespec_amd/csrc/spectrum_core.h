@@ -468,34 +468,36 @@ __device__ __forceinline__ void topk_rounds(int t, int kmin, int span, int k, XF
 // equals phi_i + 2 pi K_i with K_i the running count of +-1 corrections: K is
 // an exact integer prefix scan and u is one fma, so only the rounding of the
 // reference's running sum (not its decisions) differs.
-template <int LOG2N>
-__device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, double *scanbuf, double (&pw)[16],
-                                            double (&u)[16], double (&gd)[16]) {
+template <int LOG2N, int CH = 16>
+__device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, double *scanbuf, double (&pw)[CH],
+                                            double (&u)[CH], double (&gd)[CH]) {
+    // CH = bins per thread (16: the whole row; smaller for the top-k records, which only need the
+    // bins up to the scan range: CH * TPW >= kmax + 2, chosen at run time by the caller)
     using G = Geo<LOG2N>;
     constexpr int M = G::M, TPW = G::TPW;
     constexpr double kPi = 3.14159265358979323846;  // M_PI
     constexpr double k2Pi = 2.0 * kPi;              // the reference's 2.0 * M_PI correction
-    const int k0 = 16 * t;
-    double ph[18];  // bins k0 - 1 .. k0 + 16
+    const int k0 = CH * t;
+    double ph[CH + 2];  // bins k0 - 1 .. k0 + CH
 #pragma unroll
-    for (int j = 0; j < 18; ++j) {
+    for (int j = 0; j < CH + 2; ++j) {
         const int k = k0 - 1 + j;
         ph[j] = 0.0;  // bin M: the zeroed upper half, atan2(0, 0) = 0
         if (k >= 0 && k < M) {
             const cpx<double> x = xrow[pad16(k)];
             ph[j] = atan2(x.im, x.re);
-            if (j >= 1 && j <= 16) pw[j - 1] = x.re * x.re + x.im * x.im;
+            if (j >= 1 && j <= CH) pw[j - 1] = x.re * x.re + x.im * x.im;
         }
     }
-    int cj[17];  // correction count of bins k0 .. k0 + 16 (UnwrapPhase :1068-1077)
+    int cj[CH + 1];  // correction count of bins k0 .. k0 + CH (UnwrapPhase :1068-1077)
 #pragma unroll
-    for (int j = 0; j < 17; ++j) {
+    for (int j = 0; j < CH + 1; ++j) {
         const double diff = ph[j + 1] - ph[j];
         cj[j] = (k0 + j == 0) ? 0 : diff > kPi ? -1 : diff < -kPi ? 1 : 0;
     }
     int sum = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) sum += cj[j];
+    for (int j = 0; j < CH; ++j) sum += cj[j];
     constexpr int SW = TPW < 64 ? TPW : 64;
     const int lt = t & (SW - 1);
     int incl = sum;
@@ -513,14 +515,14 @@ __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, doub
     }
     const double um1 = fma((double)K, k2Pi, ph[0]);  // u[k0 - 1]
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < CH; ++j) {
         K += cj[j];
         u[j] = fma((double)K, k2Pi, ph[j + 1]);
     }
-    const double up16 = fma((double)(K + cj[16]), k2Pi, ph[17]);  // u[k0 + 16]
+    const double upc = fma((double)(K + cj[CH]), k2Pi, ph[CH + 1]);  // u[k0 + CH]
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {  // :1102-1119 (n = N >= 32: every bin < M has two neighbours but bin 0)
-        const double lo = j ? u[j - 1] : um1, hi = j < 15 ? u[j + 1] : up16;
+    for (int j = 0; j < CH; ++j) {  // :1102-1119 (n = N >= 32: every bin < M has two neighbours but bin 0)
+        const double lo = j ? u[j - 1] : um1, hi = j < CH - 1 ? u[j + 1] : upc;
         double g = (k0 + j == 0) ? -(u[1] - u[0]) : -(hi - lo) / 2.0;
         if (g > 100.0) g = 100.0;
         if (g < -100.0) g = -100.0;
@@ -908,7 +910,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         }
         // unwrapped phase / group delay of bins [16t, 16t + 16) (kept in registers
         // through the top-k scan for kOutTopKPhase)
-        double pw[kPhase ? 16 : 1], u[kPhase ? 16 : 1], gd[kPhase ? 16 : 1];
+        double pw[OUT == kOutPhase ? 16 : 1], u[OUT == kOutPhase ? 16 : 1], gd[OUT == kOutPhase ? 16 : 1];
         if constexpr (OUT == kOutPhase) {
             const cpx<double> *xrow = reinterpret_cast<const cpx<double> *>(lbase);
             __syncthreads();  // X row complete
@@ -1034,23 +1036,34 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 // phases of the (unmodified) X row, then the owner of each winner's chunk adds
                 // [unwrapped phase, group delay] to that slot
                 __syncthreads();  // winners list complete
-                phase_chunk<LOG2N>(reinterpret_cast<const cpx<double> *>(lbase), t, scanbuf, pw, u, gd);
-                const int nk = a.topk < KW ? a.topk : KW;
-                for (int s2 = 0; s2 < nk; ++s2) {
-                    const int b = win[s2];
-                    if (b != kNone && (b >> 4) == t && active) {
-                        double ub = 0.0, gb = 0.0;
+                // only bins 0 .. kmax + 1 feed the winners' unwrapped phase and group delay: CH bins per
+                // thread with CH * TPW >= kmax + 2 (wave-uniform choice) instead of the whole row
+                auto add_phase = [&](auto chv) {
+                    constexpr int CH = decltype(chv)::value;
+                    double pwc[CH], uc[CH], gdc[CH];
+                    phase_chunk<LOG2N, CH>(reinterpret_cast<const cpx<double> *>(lbase), t, scanbuf, pwc, uc, gdc);
+                    const int nk = a.topk < KW ? a.topk : KW;
+                    for (int s2 = 0; s2 < nk; ++s2) {
+                        const int b = win[s2];
+                        if (b != kNone && b / CH == t && active) {
+                            double ub = 0.0, gb = 0.0;
 #pragma unroll
-                        for (int j = 0; j < 16; ++j)
-                            if ((b & 15) == j) {
-                                ub = u[j];
-                                gb = gd[j];
-                            }
-                        T *rec = recw + RW * s2;
-                        rec[4] = ub;
-                        rec[5] = gb;
+                            for (int j = 0; j < CH; ++j)
+                                if (b % CH == j) {
+                                    ub = uc[j];
+                                    gb = gdc[j];
+                                }
+                            T *rec = recw + RW * s2;
+                            rec[4] = ub;
+                            rec[5] = gb;
+                        }
                     }
-                }
+                };
+                const int need = a.kmax + 2;  // bins 0 .. kmax + 1
+                if (need <= 2 * TPW) add_phase(std::integral_constant<int, 2>{});
+                else if (need <= 4 * TPW) add_phase(std::integral_constant<int, 4>{});
+                else if (need <= 8 * TPW) add_phase(std::integral_constant<int, 8>{});
+                else add_phase(std::integral_constant<int, 16>{});
             }
         }
         if constexpr (OUT == kOutPower && !kDirect) {

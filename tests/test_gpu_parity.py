@@ -389,7 +389,9 @@ def test_phase_output(gpu_session, n, detrend, period):
 
 
 @pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),
-                                               (16384, 4000, 8, 18, 52)])
+                                               (16384, 4000, 8, 18, 52),
+                                               # bins per thread of the phase scan (2/4/8/16 by kmax): CH = 8, 16, 8
+                                               (4096, 4096, 8, 6, 200), (4096, 4096, 5, 3, 300), (2048, 1, 8, 5, 100)])
 def test_topk_phase(gpu_session, n, hop, k, minp, maxp):
     """MTB_OUT_TOPK_PHASE: top-k records + unwrapped phase / group delay at each chosen bin (the
     values ComputeETA_RealFFT / CalculateScientificETASeconds read, 1.0.4-new.mq5:1165, :1239)."""
