@@ -2,23 +2,41 @@
 """bench.py -- windows/s of the MI355X spectrum hot path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config north_star]
+                    [--scaling weak|strong]
 
 One step = one launch of the hot path over the configuration's whole window
-batch, input already resident in HBM (series generated on device).  N > 1 is
-launched by torch.distributed.run: every rank owns a full, independent batch
-on its own GPU (weak scaling, no data-path collective; a CPU gloo group only
-brackets the timed region with barriers and takes the max time over ranks).
+batch, input already resident in HBM (series generated on device).  One
+process per GPU: with --gpus N > 1 and no WORLD_SIZE in the environment the
+script starts `torch.distributed.run` with N ranks as a child process (before
+any GPU call) and exits with its status; under torchrun WORLD_SIZE must equal
+--gpus.  A CPU gloo group only brackets the timed region with barriers and
+takes the max time over ranks -- no collective is on the data path (windows
+shard with no exchange).
+
+  --scaling weak   every rank owns a full, independent batch (seed per rank)
+  --scaling strong the configuration's one batch is split over the ranks:
+                   contiguous window ranges with the N - hop halo (north star,
+                   C3, C4) or whole symbols balanced by bytes (C5)
+
+Before the W warm-up steps the step is repeated until its HIP-event duration
+is steady (the MI355X holds its memory clocks low after idle and needs ~40
+launches of this size to ramp; a short timed region otherwise measures the
+ramp -- scripts/step_trace.py, profiles/r02/step_trace_*.json).  That settle
+phase is untimed and reported in the line ("settle").  The timed region is
+exactly K full steps; `roofline.kernel_ms` comes from HIP events recorded on
+the launch stream around those same K steps.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
-`roofline` (live HIP-event kernel time vs HBM peak) and `cpu_baseline` (the
-oracle -- CPU restatement of the reference path -- timed on a bounded sample
-on this host).
+`roofline` and `cpu_baseline` (the oracle -- CPU restatement of the reference
+path -- timed on a bounded sample on this host).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -31,23 +49,43 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "FFT-windows/sec"
+CONFIGS = ["c2", "c3", "north_star", "c4", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse", "large",
+           "large_262144"]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="north_star",
-                    choices=["c2", "c3", "north_star", "c4", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse", "large",
-                             "large_262144"])
+    ap.add_argument("--config", default="north_star", choices=CONFIGS)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print every rank's shard of the batch and exit, without touching a GPU (CPU tests)")
+    return ap.parse_args(argv)
 
 
 def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 outside torchrun: one process per GPU via torch.distributed.run, started as a
+    child (this process has not touched the GPU), returning its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve())] + argv
+    return subprocess.call(cmd)
 
 
 class Control:
@@ -64,41 +102,65 @@ class Control:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, v: float) -> float:
-        if self.world == 1:
-            return v
+    def _reduce(self, v: float, op) -> float:
         import torch
         t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max(self, v: float) -> float:
+        return v if self.world == 1 else self._reduce(v, self.dist.ReduceOp.MAX)
+
     def sum(self, v: float) -> float:
-        if self.world == 1:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return v if self.world == 1 else self._reduce(v, self.dist.ReduceOp.SUM)
 
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
 
 
-def timed_steps(step, sync, ctl: Control, steps: int, warmup: int) -> float:
-    """W untimed steps, then K steps bracketed by barrier + device sync; returns max seconds over ranks."""
+def timed_steps(step, sync, ctl: Control, steps: int, warmup: int, events=None) -> float:
+    """W untimed steps, then K steps bracketed by barrier + device sync; returns max seconds over
+    ranks.  `events` = (start, end, stream): HIP events recorded on the launch stream around the
+    same K steps."""
     for _ in range(warmup):
         step()
     sync()
     ctl.barrier()
     sync()
     t0 = time.perf_counter()
+    if events:
+        events[0].record(events[2])
     for _ in range(steps):
         step()
+    if events:
+        events[1].record(events[2])
     sync()
     ctl.barrier()
     t1 = time.perf_counter()
     return ctl.max(t1 - t0)
+
+
+def settle(step, stream, min_launches=8, max_ms=600.0, tol=0.03) -> dict:
+    """Repeat `step` until the last 8 launches' HIP-event durations agree within `tol` (or max_ms of
+    GPU time).  Untimed; returns what it did for the JSON line."""
+    import torch
+    durs = []
+    t0 = time.perf_counter()
+    while True:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        b.synchronize()
+        durs.append(a.elapsed_time(b))
+        last = durs[-min_launches:]
+        if len(durs) >= min_launches and max(last) <= (1 + tol) * min(last):
+            break
+        if sum(durs) >= max_ms:
+            break
+    return {"launches": len(durs), "ms": round(sum(durs), 2), "first_ms": round(durs[0], 4),
+            "last_ms": round(durs[-1], 4), "wall_s": round(time.perf_counter() - t0, 3)}
 
 
 def cpu_model() -> str:
@@ -175,135 +237,198 @@ def load_traffic(config: str):
         return None
 
 
-def run_c5(args, rank, local_rank, world, ctl):
-    """C5: 28 symbols x 20000 bars, N in {512,1024,2048,4096} (7 symbols each),
-    hop = 1, fp64, Hann -- the WaveCyclesBatchFetcher shape
-    (WaveCyclesBatchFetcher.mq5:106-133: one batch per symbol).  One step =
-    every symbol's batch; each window length runs on its own stream."""
-    import torch
-    from wavespec_amd import bridge, synth
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
-    bars, lens = 20000, (512, 1024, 2048, 4096)
-    streams = [torch.cuda.Stream(dev) for _ in lens]
-    jobs = []  # (plan, series, out, stream)
-    for sym in range(28):
-        n = lens[sym // 7]
-        nw = bars - n + 1
-        series = synth.random_walk_torch(bars, 100 + sym + 1000 * rank, dev)
-        out = torch.empty(nw * (n // 2), dtype=torch.float64, device=dev)
-        jobs.append((bridge.Plan(local_rank, n, 1, nw, "none", "hann"), series, out, streams[sym // 7]))
-    total_w = sum(j[0].n_windows for j in jobs)
-    alg = sum(j[0].algorithmic_bytes for j in jobs)
-    main_stream = torch.cuda.current_stream(dev)
+class Workload:
+    """What one rank runs: step() enqueues one step on `stream`; `windows` / `alg_bytes` are this
+    rank's per step."""
+    stream = None
+    windows = 0
+    alg_bytes = 0
+    describe = ""
+    cpu_cfg = None      # (series tensor, cfg) for the CPU baseline
+    traffic = None      # PMC HBM bytes per step, from profiles/traffic.json
 
-    def step():
-        for st in streams:
-            st.wait_stream(main_stream)
-        for plan, series, out, st in jobs:
-            plan.execute(series.data_ptr(), out.data_ptr(), st.cuda_stream)
-        for st in streams:
-            main_stream.wait_stream(st)
+    def step(self):
+        raise NotImplementedError
 
-    secs = timed_steps(step, torch.cuda.synchronize, ctl, args.steps, args.warmup)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
-    ev0.record(main_stream)
-    for _ in range(reps):
-        step()
-    ev1.record(main_stream)
-    ev1.synchronize()
-    step_s = ev0.elapsed_time(ev1) / 1e3 / reps
-    value = ctl.sum(float(total_w * args.steps)) / secs
-    baseline = baseline_all = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        plan0, s0, _, _ = jobs[-1]  # a 4096-pt symbol: the costliest per window
-        c5cfg = {"n": 4096, "hop": 1, "windows": plan0.n_windows, "detrend": "none", "window": "hann"}
-        baseline = cpu_baseline(s0, c5cfg, args.cpu_seconds)
-        baseline_all = cpu_baseline(s0, c5cfg, args.cpu_seconds / 2, cpu_threads())
-    if rank == 0:
-        achieved = alg / step_s / 1e9
+    def close(self):
+        pass
+
+
+def shard_plan(name: str, rank: int, world: int, scaling: str) -> dict:
+    """This rank's part of a configuration: windows [w0, w0+nw) and series samples [a, b) (the
+    N - hop halo included) of one batch (strong), or a whole batch of its own (weak); for C5 the
+    symbols it owns."""
+    from wavespec_amd import sharding, synth
+    if name == "c5":
+        bars, lens = 20000, (512, 1024, 2048, 4096)
+        nwins = [bars - lens[s // 7] + 1 for s in range(28)]
+        owned = (sharding.shard_symbols([nw * lens[s // 7] // 2 for s, nw in enumerate(nwins)], world, rank)
+                 if scaling == "strong" else list(range(28)))
+        return {"rank": rank, "symbols": owned, "windows": sum(nwins[s] for s in owned),
+                "seed_offset": 0 if scaling == "strong" else 1000 * rank}
+    cfg = synth.CONFIGS[name]
+    w, n, hop = cfg["windows"], cfg["n"], cfg["hop"]
+    if scaling == "strong":
+        w0, nw = sharding.shard_windows(w, world, rank)
+        seed = cfg["seed"]
+    else:
+        w0, nw, seed = 0, w, cfg["seed"] + 1000 * rank
+    a, b = (w0 * n, (w0 + nw) * n) if cfg.get("output") == "inverse" else sharding.shard_series_slice(w0, nw, hop, n)
+    return {"rank": rank, "w0": w0, "windows": nw, "series": [a, b], "seed": seed, "of": w}
+
+
+class SingleBatch(Workload):
+    """One plan over one window batch (every config but C5)."""
+
+    def __init__(self, name, rank, local_rank, world, scaling):
+        import torch
+        from wavespec_amd import bridge, synth
+        cfg = dict(synth.CONFIGS[name])
+        cfg.setdefault("trend_period", 0)
+        dev = torch.device("cuda", local_rank)
+        n, hop, w = cfg["n"], cfg["hop"], cfg["windows"]
+        f32 = cfg["precision"] == "f32"
+        tdt = torch.float32 if f32 else torch.float64
+        output = cfg.get("output", "power")
+        sp = shard_plan(name, rank, world, scaling)  # this rank's window range (+ halo) or its own batch
+        w0, nw, seed = sp["w0"], sp["windows"], sp["seed"]
+        a, b = sp["series"]
+        if nw <= 0:
+            raise SystemExit(f"rank {rank}: no windows to own ({w} windows over {world} ranks)")
+        if output == "inverse":  # rows of packed spectra (random, resident in HBM)
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(seed)
+            full = torch.randn(w * n, dtype=tdt, device=dev, generator=gen)
+            self.series = full[a:b].contiguous() if (a, b) != (0, full.numel()) else full
+            self.plan = bridge.Plan.inverse(local_rank, n, nw)
+        else:
+            full = synth.random_walk_torch((w - 1) * hop + n, seed, dev, tdt)  # resident in HBM
+            self.series = full[a:b].contiguous() if (a, b) != (0, full.numel()) else full
+            self.plan = bridge.Plan(local_rank, n, hop, nw, cfg["detrend"], cfg["window"], cfg["trend_period"],
+                                    cfg["precision"], output)
+            if output in ("topk", "topk_phase"):
+                self.plan.set_topk(8, 18.0, 200.0)  # the reference's scan (1.1.0:22-23)
+        del full
+        self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
+        self.stream = torch.cuda.current_stream(dev)
+        self._sptr = self.stream.cuda_stream
+        self._args = (self.series.data_ptr(), self.out.data_ptr(), self._sptr)
+        self.windows = nw
+        self.alg_bytes = self.plan.algorithmic_bytes
+        self.f32 = f32
+        self.cfg = cfg
+        self.cpu_cfg = (self.series, cfg)
+        self.traffic = load_traffic(name)
+        shard = f", windows [{w0}, {w0 + nw}) of {w}" if scaling == "strong" else ""
+        self.describe = (f"{name}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, {cfg['detrend']} detrend, "
+                         f"{cfg['window']} window, " + {
+                             "power": "|X|^2 k<N/2", "topk": "top-8 bins in periods [18, 200]",
+                             "phase": "[|X|^2, unwrapped phase, group delay] k<N/2",
+                             "topk_phase": "top-8 bins + phase/delay in periods [18, 200]",
+                             "inverse": "inverse real FFT of packed spectra"}[output] + shard)
+        self.n, self.hop = n, hop
+
+    def step(self):
+        self.plan.execute(*self._args)
+
+    def close(self):
+        self.plan.close()
+
+
+class C5Batch(Workload):
+    """C5: 28 symbols x 20000 bars, N in {512,1024,2048,4096} (7 symbols each), hop = 1, fp64,
+    Hann -- the WaveCyclesBatchFetcher shape (WaveCyclesBatchFetcher.mq5:106-133: one batch per
+    symbol).  One step = every owned symbol's batch; each window length runs on its own stream,
+    joined into the launch stream."""
+
+    def __init__(self, rank, local_rank, world, scaling):
+        import torch
+        from wavespec_amd import bridge, synth
+        dev = torch.device("cuda", local_rank)
+        bars, lens = 20000, (512, 1024, 2048, 4096)
+        nwins = [bars - lens[s // 7] + 1 for s in range(28)]
+        sp = shard_plan("c5", rank, world, scaling)
+        owned, seed_off = sp["symbols"], sp["seed_offset"]
+        self.streams = [torch.cuda.Stream(dev) for _ in lens]
+        self.jobs = []  # (plan, series, out, stream)
+        for sym in owned:
+            n = lens[sym // 7]
+            series = synth.random_walk_torch(bars, 100 + sym + seed_off, dev)
+            out = torch.empty(nwins[sym] * (n // 2), dtype=torch.float64, device=dev)
+            self.jobs.append((bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann"), series, out,
+                              self.streams[sym // 7]))
+        self.stream = torch.cuda.current_stream(dev)
+        self.windows = sum(j[0].n_windows for j in self.jobs)
+        self.alg_bytes = sum(j[0].algorithmic_bytes for j in self.jobs)
         per_launch = load_traffic("c5")  # PMC bytes per spectrum dispatch; one step is len(jobs) dispatches
-        c5_traffic = per_launch * len(jobs) if per_launch else None
-        print(json.dumps({
-            "metric": METRIC, "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (28 random-walk symbols generated on device)",
-            "config": {"workload": f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2",
-                       "windows_per_gpu": total_w, "window_len": "mixed", "hop": 1,
-                       "parallelism": f"symbols' batches on 4 streams, x{world} GPUs"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": c5_traffic,
-                         "algorithmic_bytes_per_launch": alg, "kernel_ms": step_s * 1e3,
-                         "note": "one step = 28 launches on 4 streams; time per step from HIP events"},
-            "cpu_baseline": baseline, "cpu_baseline_all_cores": baseline_all}), flush=True)
-    for j in jobs:
-        j[0].close()
-    ctl.close()
+        self.traffic = per_launch * len(self.jobs) if per_launch else None
+        self.f32 = False
+        big = [j for j in self.jobs if j[0].window_len == 4096]
+        if big:  # a 4096-pt symbol: the costliest per window
+            p0, s0 = big[-1][0], big[-1][1]
+            self.cpu_cfg = (s0, {"n": 4096, "hop": 1, "windows": p0.n_windows, "detrend": "none", "window": "hann"})
+        self.describe = (f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2"
+                         + (f", {len(owned)} symbols on this rank" if scaling == "strong" else ""))
+
+    def step(self):
+        for st in self.streams:
+            st.wait_stream(self.stream)
+        for plan, series, out, st in self.jobs:
+            plan.execute(series.data_ptr(), out.data_ptr(), st.cuda_stream)
+        for st in self.streams:
+            self.stream.wait_stream(st)
+
+    def close(self):
+        for j in self.jobs:
+            j[0].close()
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     rank, local_rank, world = dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+    if args.plan_only:
+        ctl = Control(world)
+        mine = shard_plan(args.config, rank, world, args.scaling)
+        parts = [mine]
+        if world > 1:
+            parts = [None] * world
+            ctl.dist.all_gather_object(parts, mine)
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "config": args.config, "scaling": args.scaling, "shards": parts}),
+                  flush=True)
+        ctl.close()
+        return 0
     import torch
-    from wavespec_amd import bridge, synth
 
-    if args.config == "c5":
-        return run_c5(args, rank, local_rank, world, Control(world))
-    cfg = dict(synth.CONFIGS[args.config])
-    cfg.setdefault("trend_period", 0)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     ctl = Control(world)
-
-    n, hop, w = cfg["n"], cfg["hop"], cfg["windows"]
-    f32 = cfg["precision"] == "f32"
-    tdt = torch.float32 if f32 else torch.float64
-    length = (w - 1) * hop + n
-    output = cfg.get("output", "power")
-    if output == "inverse":  # rows of packed spectra (random, resident in HBM)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(cfg["seed"] + 1000 * rank)
-        d_series = torch.randn(w * n, dtype=tdt, device=dev, generator=gen)
-        plan = bridge.Plan.inverse(local_rank, n, w)
+    if args.config == "c5":
+        wl = C5Batch(rank, local_rank, world, args.scaling)
     else:
-        d_series = synth.random_walk_torch(length, cfg["seed"] + 1000 * rank, dev, tdt)  # resident in HBM
-        plan = bridge.Plan(local_rank, n, hop, w, cfg["detrend"], cfg["window"], cfg["trend_period"],
-                           cfg["precision"], output)
-        if output in ("topk", "topk_phase"):
-            plan.set_topk(8, 18.0, 200.0)  # the reference's scan (1.1.0:22-23)
-    d_out = torch.empty(w * plan.record, dtype=tdt, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling)
+    torch.cuda.synchronize()
 
-    def step():
-        plan.execute(d_series.data_ptr(), d_out.data_ptr(), sptr)
+    settled = None if args.no_settle else settle(wl.step, wl.stream)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), wl.stream)
+    secs = timed_steps(wl.step, torch.cuda.synchronize, ctl, args.steps, args.warmup, ev)
+    kernel_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps  # this rank, same K steps, launch stream
+    kernel_s_max = ctl.max(kernel_s)
+    achieved = wl.alg_bytes / kernel_s / 1e9
 
-    sync = torch.cuda.synchronize
-    secs = timed_steps(step, sync, ctl, args.steps, args.warmup)
-
-    # live kernel time with HIP events on the launch stream (roofline)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = max(10, min(args.steps, 50))
-    ev0.record(stream)
-    for _ in range(reps):
-        step()
-    ev1.record(stream)
-    ev1.synchronize()
-    kernel_s = ev0.elapsed_time(ev1) / 1e3 / reps
-    alg_bytes = plan.algorithmic_bytes
-    achieved = alg_bytes / kernel_s / 1e9
-
-    total_windows = ctl.sum(float(w * args.steps))
+    total_windows = ctl.sum(float(wl.windows * args.steps))
     value = total_windows / secs
     baseline = baseline_all = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baseline = cpu_baseline(d_series, cfg, args.cpu_seconds)
-        baseline_all = cpu_baseline(d_series, cfg, args.cpu_seconds / 2, cpu_threads())
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.cpu_cfg is not None:
+        baseline = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], args.cpu_seconds)
+        baseline_all = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], args.cpu_seconds / 2, cpu_threads())
 
     if rank == 0:
-        traffic = load_traffic(args.config)
         line = {
             "metric": METRIC,
             "value": value,
@@ -313,27 +438,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": secs / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "f32" if f32 else "f64",
+            "dtype": "f32" if wl.f32 else "f64",
             "data": "synthetic (random-walk close prices generated on device, seed per rank)",
-            "config": {"workload": f"{args.config}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, "
-                                   f"{cfg['detrend']} detrend, {cfg['window']} window, " + {
-                                       "power": "|X|^2 k<N/2", "topk": "top-8 bins in periods [18, 200]",
-                                       "phase": "[|X|^2, unwrapped phase, group delay] k<N/2",
-                                       "topk_phase": "top-8 bins + phase/delay in periods [18, 200]",
-                                       "inverse": "inverse real FFT of packed spectra"}[output],
-                       "windows_per_gpu": w, "window_len": n, "hop": hop, "parallelism": f"windows sharded x{world}"},
+            "config": {"workload": wl.describe, "windows_per_gpu": wl.windows, "windows_total": int(total_windows / args.steps),
+                       "parallelism": f"windows sharded x{world} ({args.scaling}), no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_s * 1e3},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
+                         "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,
+                         "kernel_ms_max_over_ranks": kernel_s_max * 1e3,
+                         "timing": "HIP events on the launch stream around the same K timed steps (rank 0)"},
+            "settle": settled,
             "cpu_baseline": baseline,
             "cpu_baseline_all_cores": baseline_all,
         }
         print(json.dumps(line), flush=True)
-    plan.close()
+    wl.close()
     ctl.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

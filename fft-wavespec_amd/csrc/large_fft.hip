@@ -517,11 +517,7 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
 }  // namespace
 
 int64_t large_chunk(int log2n, bool f32) {
-    static const int64_t mb = [] {
-        const char *e = getenv("WSP_LARGE_CHUNK_MB");
-        const int64_t v = e ? atoll(e) : 0;
-        return v > 0 ? v : int64_t(192);
-    }();
+    constexpr int64_t mb = 192;  // measured best of 16..2048 MiB (profiles/r01/large_chunk_sweep.log)
     const int64_t per = (int64_t(1) << (log2n - 1)) * (f32 ? 8 : 16);
     const int64_t c = (mb << 20) / per;
     return c < 1 ? 1 : c;

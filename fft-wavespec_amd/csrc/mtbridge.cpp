@@ -76,6 +76,7 @@ struct Pool {
     std::mutex mu;
     std::map<std::pair<int, size_t>, std::vector<void *>> free_dev;  // (device, bytes)
     std::map<size_t, std::vector<void *>> free_host;
+    std::map<int, std::vector<hipEvent_t>> free_events;              // per device, timing disabled
 };
 Pool &pool() {
     static Pool *p = new Pool();  // intentionally leaked: no teardown after the HIP runtime
@@ -128,6 +129,30 @@ void host_free(void *p, size_t bytes) {
     std::lock_guard<std::mutex> lk(pool().mu);
     pool().free_host[bucket_bytes(bytes)].push_back(p);
 }
+// Completion events of batch parts: recycled, so that a per-bar call creates
+// none (hipEventCreate costs a driver round trip).
+hipEvent_t event_alloc(int dev) {
+    {
+        std::lock_guard<std::mutex> lk(pool().mu);
+        auto &v = pool().free_events[dev];
+        if (!v.empty()) {
+            hipEvent_t e = v.back();
+            v.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipSetDevice(dev) != hipSuccess || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        set_error("hipEventCreateWithFlags failed on device %d", dev);
+        return nullptr;
+    }
+    return e;
+}
+void event_free(int dev, hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().free_events[dev].push_back(e);
+}
 void pool_release_all() {
     std::lock_guard<std::mutex> lk(pool().mu);
     for (auto &kv : pool().free_dev) {
@@ -138,6 +163,11 @@ void pool_release_all() {
     for (auto &kv : pool().free_host)
         for (void *p : kv.second) (void)hipHostFree(p);
     pool().free_host.clear();
+    for (auto &kv : pool().free_events) {
+        (void)hipSetDevice(kv.first);
+        for (hipEvent_t e : kv.second) (void)hipEventDestroy(e);
+    }
+    pool().free_events.clear();
 }
 
 // ----------------------------------------------------------------- tables
@@ -374,11 +404,6 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         K.n = c.n;
         K.f32 = c.f32;
         memcpy(K.params, kalman, sizeof(K.params));
-        static const int kvar = [] {  // ablation override: WSP_KALMAN_SPREAD=0 -> single-wave workgroups
-            const char *e = getenv("WSP_KALMAN_SPREAD");
-            return e && atoi(e) == 0 ? 1 : 0;
-        }();
-        K.variant = kvar;
         HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
         L.series = d_ws;
         L.hop = c.n;
@@ -411,18 +436,66 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
 }
 
 // ------------------------------------------------------------------ session
+// A DeviceCtx owns its streams: they are destroyed with it, i.e. when the
+// last holder of the Session (an in-flight call on another thread, or the
+// session table) lets it go -- never under a call that still enqueues on them.
 struct DeviceCtx {
     int dev = 0;
     std::vector<hipStream_t> streams;
     std::atomic<unsigned> rr{0};
     hipStream_t next_stream() { return streams[rr.fetch_add(1) % streams.size()]; }
+    ~DeviceCtx() {
+        if (streams.empty()) return;
+        (void)hipSetDevice(dev);
+        for (auto st : streams) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    }
 };
+
+// Per-bar single-window path (gpu_fft_real_forward, 1.1.0:1249 -> :520): a
+// private stream plus device-mapped pinned buffers.  The kernel reads the
+// window from and writes the packed spectrum to host memory directly (8-32
+// KiB over PCIe), so one call is one kernel launch and one stream sync, with
+// no DMA copies and no allocation.  Contexts are checked out per call, so
+// concurrent callers (one thread per chart) never share one.
+struct LiveCtx {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    double *h_in = nullptr, *h_out = nullptr;  // pinned, device-mapped
+    double *d_in = nullptr, *d_out = nullptr;  // their device addresses
+    int cap = 0;                               // doubles per buffer
+    ~LiveCtx() {
+        (void)hipSetDevice(dev);
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (h_in) (void)hipHostFree(h_in);
+        if (h_out) (void)hipHostFree(h_out);
+    }
+};
+
 struct Session {
     int device_index = 0;
     std::vector<std::unique_ptr<DeviceCtx>> devs;
+    std::mutex live_mu;
+    std::vector<std::unique_ptr<LiveCtx>> live_free;
 };
+
+// Session lifetime (SURVEY 8b "per-session refcount"): every successful
+// gpu_init adds a reference, every gpu_shutdown drops one; the session is torn
+// down only when the count reaches zero.  In MT5 each chart calls gpu_init
+// once (EnsureGpu, 1.1.0:722-751) and gpu_shutdown once (OnDeinit,
+// 1.1.0:706-716), and all charts share one process: closing one chart must not
+// end the others' session.  References are also counted per calling thread
+// (MT5 runs each symbol's indicators on one thread): when a thread's own count
+// drops to zero its jobs are released, other threads' jobs are left alone.
 std::mutex g_session_mu;
 std::shared_ptr<Session> g_session;
+int g_session_refs = 0;
+std::map<std::thread::id, int> *g_thread_refs = new std::map<std::thread::id, int>();
 
 std::shared_ptr<Session> session() {
     std::lock_guard<std::mutex> lk(g_session_mu);
@@ -436,6 +509,7 @@ struct Part {
     int dev = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    bool recorded = false;  // `done` follows every command of the part
     int64_t w0 = 0, nw = 0;
     void *d_in = nullptr, *d_out = nullptr, *d_ws = nullptr;
     size_t in_bytes = 0, out_bytes = 0, ws_bytes = 0;
@@ -450,11 +524,10 @@ struct Batch {
     std::string error;
     ~Batch() {
         for (auto &p : parts) {
-            if (p.done) {
-                (void)hipSetDevice(p.dev);
-                (void)hipEventSynchronize(p.done);
-                (void)hipEventDestroy(p.done);
-            }
+            (void)hipSetDevice(p.dev);
+            if (p.recorded) (void)hipEventSynchronize(p.done);
+            else if (p.stream) (void)hipStreamSynchronize(p.stream);  // a part abandoned mid-enqueue
+            event_free(p.dev, p.done);
             dev_free(p.dev, p.d_in, p.in_bytes);
             dev_free(p.dev, p.d_out, p.out_bytes);
             dev_free(p.dev, p.d_ws, p.ws_bytes);
@@ -550,7 +623,8 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             P.d_out = dev_alloc(P.dev, P.out_bytes);
             if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
             if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
-            HIP_OR(hipEventCreateWithFlags(&P.done, hipEventDisableTiming), MTB_INTERNAL_ERROR);
+            P.done = event_alloc(P.dev);
+            if (!P.done) return MTB_INTERNAL_ERROR;
             const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
             if (e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
                 stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
@@ -563,6 +637,7 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             char *dst = (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
             HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
             HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+            P.recorded = true;
         }
     }
     *out = std::move(b);
@@ -626,20 +701,116 @@ int run_sync(const Config &c, const double *series, double *out, int64_t out_cap
 }
 
 // --------------------------------------------------------------------- jobs
+// The table only maps ids to batches; a caller copies the shared_ptr out
+// under the lock and polls / copies results with the lock released, so one
+// chart's multi-GB copy-out never blocks another chart's submit or poll, and
+// gpu_free_job during a copy-out only drops the table's reference.
+struct Job {
+    std::shared_ptr<Batch> batch;
+    std::thread::id owner;  // submitting thread: its gpu_shutdown releases the job
+};
 std::mutex g_jobs_mu;
-std::map<int64_t, std::unique_ptr<Batch>> *g_jobs = new std::map<int64_t, std::unique_ptr<Batch>>();
+std::map<int64_t, Job> *g_jobs = new std::map<int64_t, Job>();
 std::atomic<int64_t> g_next_id{1};
 
+std::shared_ptr<Batch> find_job(int64_t id) {
+    std::lock_guard<std::mutex> lk(g_jobs_mu);
+    auto it = g_jobs->find(id);
+    return it == g_jobs->end() ? nullptr : it->second.batch;
+}
+
+// Removes the jobs of one thread (all threads when `all`); the batches are
+// destroyed (waiting for their device work) after the lock is released.
+void release_jobs(bool all, std::thread::id owner) {
+    std::vector<std::shared_ptr<Batch>> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_jobs_mu);
+        for (auto it = g_jobs->begin(); it != g_jobs->end();) {
+            if (all || it->second.owner == owner) {
+                drop.push_back(std::move(it->second.batch));
+                it = g_jobs->erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+}
+
 // -------------------------------------------------------------------- plans
+// Plans are shared: wsp_plan_execute holds a reference while it enqueues, so
+// a concurrent wsp_plan_destroy cannot free the workspace under it (the last
+// reference frees it, after the device has finished with it), and cfg is
+// read and written under the plan's own mutex (wsp_plan_set_topk).
 struct Plan {
     int dev = 0;
+    std::mutex mu;
     Config cfg;
     double kalman[16];
     void *d_ws = nullptr;
     size_t ws_bytes = 0;
+    ~Plan() {
+        if (d_ws) {
+            (void)hipSetDevice(dev);
+            (void)hipDeviceSynchronize();
+            (void)hipFree(d_ws);
+        }
+    }
 };
 std::mutex g_plans_mu;
-std::map<int64_t, std::unique_ptr<Plan>> *g_plans = new std::map<int64_t, std::unique_ptr<Plan>>();
+std::map<int64_t, std::shared_ptr<Plan>> *g_plans = new std::map<int64_t, std::shared_ptr<Plan>>();
+
+std::shared_ptr<Plan> find_plan(int64_t id) {
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    auto it = g_plans->find(id);
+    return it == g_plans->end() ? nullptr : it->second;
+}
+
+// ------------------------------------------------------- live single window
+std::unique_ptr<LiveCtx> live_checkout(Session &S, int n) {
+    std::unique_ptr<LiveCtx> L;
+    {
+        std::lock_guard<std::mutex> lk(S.live_mu);
+        if (!S.live_free.empty()) {
+            L = std::move(S.live_free.back());
+            S.live_free.pop_back();
+        }
+    }
+    if (!L) {
+        L = std::make_unique<LiveCtx>();
+        L->dev = S.devs[0]->dev;
+        if (hipSetDevice(L->dev) != hipSuccess ||
+            hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("live context: stream creation failed on device %d", L->dev);
+            return nullptr;
+        }
+    }
+    if (L->cap < n) {
+        (void)hipSetDevice(L->dev);
+        if (L->h_in) (void)hipHostFree(L->h_in);
+        if (L->h_out) (void)hipHostFree(L->h_out);
+        L->h_in = L->h_out = nullptr;
+        L->cap = 0;
+        void *hi = nullptr, *ho = nullptr, *di = nullptr, *dd = nullptr;
+        if (hipHostMalloc(&hi, (size_t)n * sizeof(double), hipHostMallocMapped) != hipSuccess ||
+            hipHostMalloc(&ho, (size_t)n * sizeof(double), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer(&di, hi, 0) != hipSuccess || hipHostGetDevicePointer(&dd, ho, 0) != hipSuccess) {
+            if (hi) (void)hipHostFree(hi);
+            if (ho) (void)hipHostFree(ho);
+            set_error("live context: mapped pinned buffers of %d doubles failed", n);
+            return nullptr;
+        }
+        L->h_in = static_cast<double *>(hi);
+        L->h_out = static_cast<double *>(ho);
+        L->d_in = static_cast<double *>(di);
+        L->d_out = static_cast<double *>(dd);
+        L->cap = n;
+    }
+    return L;
+}
+void live_checkin(Session &S, std::unique_ptr<LiveCtx> L) {
+    std::lock_guard<std::mutex> lk(S.live_mu);
+    S.live_free.push_back(std::move(L));
+}
 
 }  // namespace
 
@@ -650,7 +821,16 @@ MTB_API const char *wsp_version(void) { return "mtbridge-mi355x 0.1.0 gfx950"; }
 
 MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count) {
     std::lock_guard<std::mutex> lk(g_session_mu);
-    if (g_session && g_session->device_index == device_index) return MTB_OK;
+    if (g_session) {
+        if (g_session->device_index != device_index) {
+            set_error("gpu_init(%d): a session is open on device %d for %d caller(s); gpu_shutdown them first",
+                      device_index, g_session->device_index, g_session_refs);
+            return MTB_BAD_ARGS;
+        }
+        ++g_session_refs;
+        ++(*g_thread_refs)[std::this_thread::get_id()];
+        return MTB_OK;
+    }
     const int n = device_count();
     if (n <= 0) {
         set_error("no HIP device visible (hipGetDeviceCount=0); the spectrum path has no CPU fallback");
@@ -661,46 +841,56 @@ MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count) {
         return MTB_BAD_ARGS;
     }
     const int streams = std::max(1, std::min(512, (int)stream_count));
-    auto S = std::make_shared<Session>();
+    auto S = std::make_shared<Session>();  // on failure below, ~DeviceCtx destroys the streams made so far
     S->device_index = device_index;
     const int first = device_index < 0 ? 0 : device_index;
     const int last = device_index < 0 ? n - 1 : device_index;
     for (int d = first; d <= last; ++d) {
-        auto D = std::make_unique<DeviceCtx>();
-        D->dev = d;
+        S->devs.push_back(std::make_unique<DeviceCtx>());
+        DeviceCtx &D = *S->devs.back();
+        D.dev = d;
         HIP_OR(hipSetDevice(d), MTB_BACKEND_UNAVAILABLE);
-        for (int s = 0; s < streams; ++s) {
+        for (int k = 0; k < streams; ++k) {
             hipStream_t st;
             HIP_OR(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), MTB_BACKEND_UNAVAILABLE);
-            D->streams.push_back(st);
+            D.streams.push_back(st);
         }
-        S->devs.push_back(std::move(D));
     }
     g_session = S;
+    g_session_refs = 1;
+    g_thread_refs->clear();
+    (*g_thread_refs)[std::this_thread::get_id()] = 1;
     return MTB_OK;
 }
 
 MTB_API void gpu_shutdown(void) {
-    {
-        std::lock_guard<std::mutex> lk(g_jobs_mu);
-        g_jobs->clear();  // ~Batch waits for in-flight work
-    }
+    const std::thread::id me = std::this_thread::get_id();
     std::shared_ptr<Session> S;
+    bool mine = false;
     {
         std::lock_guard<std::mutex> lk(g_session_mu);
-        S = std::move(g_session);
-        g_session.reset();
-    }
-    if (S) {
-        for (auto &D : S->devs) {
-            (void)hipSetDevice(D->dev);
-            for (auto st : D->streams) {
-                (void)hipStreamSynchronize(st);
-                (void)hipStreamDestroy(st);
-            }
+        if (!g_session) return;
+        auto it = g_thread_refs->find(me);
+        if (it != g_thread_refs->end() && --it->second <= 0) {
+            g_thread_refs->erase(it);
+            mine = true;
+        } else if (it == g_thread_refs->end()) {
+            mine = true;  // a thread that holds no reference of its own: only its own jobs (if any) go
+        }
+        if (--g_session_refs <= 0) {
+            S = std::move(g_session);
+            g_session.reset();
+            g_session_refs = 0;
+            g_thread_refs->clear();
         }
     }
-    pool_release_all();
+    if (S) {
+        release_jobs(true, me);  // ~Batch waits for in-flight work
+        S.reset();               // streams go with the last holder (calls in flight keep their own reference)
+        pool_release_all();
+    } else if (mine) {
+        release_jobs(false, me);
+    }
 }
 
 MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out) {
@@ -711,8 +901,30 @@ MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out)
     Config c;
     int st = make_config(len, len, 1, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64, MTB_OUT_PACKED, &c);
     if (st != MTB_OK) return st;
-    int32_t n = 0;
-    return run_sync(c, in, out, len, &n);
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    if (c.log2n > kMaxLog2N) {  // four-step transform: needs its chunk workspace, take the batch path
+        int32_t n = 0;
+        return run_sync(c, in, out, len, &n);
+    }
+    std::unique_ptr<LiveCtx> L = live_checkout(*S, len);
+    if (!L) return MTB_NO_MEM;
+    memcpy(L->h_in, in, (size_t)len * sizeof(double));
+    st = enqueue(L->dev, c, nullptr, L->d_in, L->d_out, nullptr, L->stream);
+    if (st == MTB_OK) {
+        const hipError_t e = hipStreamSynchronize(L->stream);
+        if (e != hipSuccess) {
+            set_error("gpu_fft_real_forward: %s", hipGetErrorString(e));
+            st = MTB_INTERNAL_ERROR;
+        } else {
+            memcpy(out, L->h_out, (size_t)len * sizeof(double));
+        }
+    }
+    live_checkin(*S, std::move(L));
+    return st;
 }
 
 MTB_API int32_t gpu_fft_real_forward_batch(const double *in, int32_t window_len, int32_t n_windows, double *out) {
@@ -893,7 +1105,7 @@ MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_l
     const int64_t id = g_next_id.fetch_add(1);
     {
         std::lock_guard<std::mutex> lk(g_jobs_mu);
-        (*g_jobs)[id] = std::move(b);
+        (*g_jobs)[id] = Job{std::shared_ptr<Batch>(std::move(b)), std::this_thread::get_id()};
     }
     *job_id = id;
     return MTB_OK;
@@ -903,30 +1115,28 @@ MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t 
                                            int32_t *ready) {
     if (ready) *ready = 0;
     if (out_len) *out_len = 0;
-    std::lock_guard<std::mutex> lk(g_jobs_mu);
-    auto it = g_jobs->find(job_id);
-    if (it == g_jobs->end()) {
+    std::shared_ptr<Batch> b = find_job(job_id);  // the table lock is held only for the lookup
+    if (!b) {
         set_error("unknown job id %lld", (long long)job_id);
         return MTB_BAD_ARGS;
     }
-    Batch &b = *it->second;
-    const int st = batch_poll(b, false);
+    const int st = batch_poll(*b, false);
     if (st == MTB_NOT_READY) return MTB_NOT_READY;
     if (ready) *ready = 1;
     if (st != MTB_OK) return st;
-    if (!out || out_cap < b.cfg.record()) {
-        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)b.cfg.record());
+    if (!out || out_cap < b->cfg.record()) {
+        set_error("out_cap=%d smaller than one record (%lld doubles)", out_cap, (long long)b->cfg.record());
         return MTB_BAD_ARGS;
     }
     int32_t n = 0;
-    const int cst = batch_copy_out(b, out, out_cap, false, &n);
+    const int cst = batch_copy_out(*b, out, out_cap, false, &n);
     if (cst != MTB_OK) return cst;
     if (out_len) *out_len = n;
     return MTB_OK;
 }
 
 MTB_API int32_t gpu_free_job(int64_t job_id) {
-    std::unique_ptr<Batch> b;
+    std::shared_ptr<Batch> b;
     {
         std::lock_guard<std::mutex> lk(g_jobs_mu);
         auto it = g_jobs->find(job_id);
@@ -934,10 +1144,10 @@ MTB_API int32_t gpu_free_job(int64_t job_id) {
             set_error("unknown job id %lld", (long long)job_id);
             return MTB_BAD_ARGS;
         }
-        b = std::move(it->second);
+        b = std::move(it->second.batch);
         g_jobs->erase(it);
     }
-    return MTB_OK;  // ~Batch waits for the device and recycles buffers
+    return MTB_OK;  // the last reference's ~Batch waits for the device and recycles buffers
 }
 
 MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n) {
@@ -991,18 +1201,30 @@ MTB_API int32_t gpu_get_last_error_w(uint16_t *buf, int32_t buf_len) {
 }
 
 // ---- device-resident plans -------------------------------------------------
-MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop, int64_t n_windows, int32_t detrend,
-                                int32_t window, int32_t trend_period, int32_t precision, int32_t output) {
+static int64_t plan_register(std::shared_ptr<Plan> p) {
+    const int64_t id = g_next_id.fetch_add(1);
+    std::lock_guard<std::mutex> lk(g_plans_mu);
+    (*g_plans)[id] = std::move(p);
+    return id;
+}
+
+static bool plan_device_ok(int32_t device) {
     const int n = device_count();
     if (n <= 0) {
         set_error("no HIP device visible; the spectrum path has no CPU fallback");
-        return 0;
+        return false;
     }
     if (device < 0 || device >= n) {
         set_error("device %d out of range (%d devices)", device, n);
-        return 0;
+        return false;
     }
-    auto p = std::make_unique<Plan>();
+    return true;
+}
+
+MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop, int64_t n_windows, int32_t detrend,
+                                int32_t window, int32_t trend_period, int32_t precision, int32_t output) {
+    if (!plan_device_ok(device)) return 0;
+    auto p = std::make_shared<Plan>();
     if (make_config(window_len, hop, n_windows, detrend, window, trend_period, precision, output, &p->cfg) != MTB_OK)
         return 0;
     p->dev = device;
@@ -1015,47 +1237,33 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
     p->ws_bytes = ws_layout(p->cfg).total;
     if (p->ws_bytes) {
         if (hipSetDevice(device) != hipSuccess || hipMalloc(&p->d_ws, p->ws_bytes) != hipSuccess) {
+            p->d_ws = nullptr;
             set_error("hipMalloc(%zu) for the plan workspace failed", p->ws_bytes);
             return 0;
         }
     }
-    const int64_t id = g_next_id.fetch_add(1);
-    std::lock_guard<std::mutex> lk(g_plans_mu);
-    (*g_plans)[id] = std::move(p);
-    return id;
+    return plan_register(std::move(p));
 }
 
 MTB_API int64_t wsp_plan_create_inverse(int32_t device, int32_t window_len, int64_t n_windows) {
-    const int n = device_count();
-    if (n <= 0) {
-        set_error("no HIP device visible; the inverse path has no CPU fallback");
-        return 0;
-    }
-    if (device < 0 || device >= n) {
-        set_error("device %d out of range (%d devices)", device, n);
-        return 0;
-    }
-    auto p = std::make_unique<Plan>();
+    if (!plan_device_ok(device)) return 0;
+    auto p = std::make_shared<Plan>();
     if (make_config(window_len, window_len, n_windows, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F64,
                     MTB_OUT_PACKED, &p->cfg) != MTB_OK)
         return 0;
     p->cfg.op = kOpInverse;
+    if (p->cfg.log2n > kMaxLog2N) {
+        set_error("window_len=%d: the inverse transform covers windows up to %d", window_len, 1 << kMaxLog2N);
+        return 0;
+    }
     p->dev = device;
     Tables t;
     if (get_tables(device, p->cfg.log2n, false, &t) != MTB_OK) return 0;
-    const int64_t id = g_next_id.fetch_add(1);
-    std::lock_guard<std::mutex> lk(g_plans_mu);
-    (*g_plans)[id] = std::move(p);
-    return id;
+    return plan_register(std::move(p));
 }
 
 MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream) {
-    Plan *p = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_plans_mu);
-        auto it = g_plans->find(plan);
-        if (it != g_plans->end()) p = it->second.get();
-    }
+    std::shared_ptr<Plan> p = find_plan(plan);  // keeps the plan (and its workspace) alive through the enqueue
     if (!p) {
         set_error("unknown plan %lld", (long long)plan);
         return MTB_BAD_ARGS;
@@ -1064,33 +1272,41 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
         set_error("wsp_plan_execute: null device buffer");
         return MTB_BAD_ARGS;
     }
-    return enqueue(p->dev, p->cfg, p->kalman, d_series, d_out, p->d_ws, (hipStream_t)hip_stream);
+    Config c;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        c = p->cfg;
+    }
+    return enqueue(p->dev, c, p->kalman, d_series, d_out, p->d_ws, (hipStream_t)hip_stream);
 }
 
 MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period) {
-    std::lock_guard<std::mutex> lk(g_plans_mu);
-    auto it = g_plans->find(plan);
-    if (it == g_plans->end()) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p) {
         set_error("unknown plan %lld", (long long)plan);
         return MTB_BAD_ARGS;
     }
-    if (it->second->cfg.op != kOpSpectrum) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->cfg.op != kOpSpectrum) {
         set_error("plan %lld is not a spectrum plan", (long long)plan);
         return MTB_BAD_ARGS;
     }
-    return config_set_topk(&it->second->cfg, top_k, min_period, max_period);
+    Config c = p->cfg;  // applied only when valid
+    const int st = config_set_topk(&c, top_k, min_period, max_period);
+    if (st == MTB_OK) p->cfg = c;
+    return st;
 }
 
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan) {
-    std::lock_guard<std::mutex> lk(g_plans_mu);
-    auto it = g_plans->find(plan);
-    if (it == g_plans->end()) return -1;
-    const Config &c = it->second->cfg;
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p) return -1;
+    std::lock_guard<std::mutex> lk(p->mu);
+    const Config &c = p->cfg;
     return (c.unique_input_elems() + c.n_windows * c.record()) * (int64_t)c.elem();
 }
 
 MTB_API int32_t wsp_plan_destroy(int64_t plan) {
-    std::unique_ptr<Plan> p;
+    std::shared_ptr<Plan> p;
     {
         std::lock_guard<std::mutex> lk(g_plans_mu);
         auto it = g_plans->find(plan);
@@ -1101,12 +1317,7 @@ MTB_API int32_t wsp_plan_destroy(int64_t plan) {
         p = std::move(it->second);
         g_plans->erase(it);
     }
-    if (p->d_ws) {
-        (void)hipSetDevice(p->dev);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(p->d_ws);
-    }
-    return MTB_OK;
+    return MTB_OK;  // the last reference (here, or an execute in flight) frees the workspace
 }
 
 }  // extern "C"

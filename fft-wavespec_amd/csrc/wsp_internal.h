@@ -80,7 +80,7 @@ struct LargeLaunch {
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
-// profiles/r01/large_chunk_sweep.log; WSP_LARGE_CHUNK_MB overrides)
+// profiles/r01/large_chunk_sweep.log)
 int64_t large_chunk(int log2n, bool f32);
 
 // Per-window Kalman 4D detrend pre-pass: d[w*N + j] = x_j - trend_j

@@ -18,6 +18,7 @@
 // out.bin receives `bars` spectra of N/2 doubles, oldest window first.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -121,6 +122,7 @@ int main(int argc, char **argv) {
         return 4;
     }
     std::vector<double> spectra((size_t)bars * (N / 2));
+    std::vector<double> call_us;  // live mode: wall time of each gpu_fft_real_forward call
     const auto t0 = std::chrono::steady_clock::now();
 
     if (mode == "live") {
@@ -135,7 +137,9 @@ int main(int argc, char **argv) {
             for (int j = 0; j < N; ++j)  // BuildPlaPriceSeries 1.1.0:765-769
                 feed_data[j] = cache.close[(size_t)shift_end_feed + (N - 1 - j)];
             // FftProcessor::Run (1.1.0:518-531)
+            const auto c0 = std::chrono::steady_clock::now();
             st = br.fft(feed_data.data(), N, g_fft_interleaved.data());
+            call_us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count());
             if (st != MTB_OK) {
                 fprintf(stderr, "[harness] gpu_fft_real_forward st=%d reason=%s\n", st, br.error().c_str());
                 return 5;
@@ -188,5 +192,15 @@ int main(int argc, char **argv) {
     br.shutdown();  // OnDeinit 1.1.0:706-716
     printf("[harness] mode=%s N=%d bars=%d seconds=%.6f bars_per_s=%.1f\n", mode.c_str(), N, bars, secs,
            bars / (secs > 0 ? secs : 1e-9));
+    if (!call_us.empty()) {  // per-bar latency of the synchronous DLL call (1.1.0:1249 -> :520)
+        std::vector<double> v = call_us;
+        std::sort(v.begin(), v.end());
+        auto pct = [&](double q) { return v[std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5))]; };
+        double sum = 0.0;
+        for (double x : v) sum += x;
+        printf("[harness] gpu_fft_real_forward N=%d calls=%zu us: first=%.1f p50=%.1f p90=%.1f p99=%.1f max=%.1f "
+               "mean=%.1f\n",
+               N, v.size(), call_us[0], pct(0.5), pct(0.9), pct(0.99), v.back(), sum / (double)v.size());
+    }
     return 0;
 }

@@ -177,18 +177,23 @@ def on_calculate(cache: FeedCache, fft_window: int, bars: int, fft: FftProcessor
     Returns the (bars, N/2) spectra.  Bars whose GPU call fails are skipped
     with NaN rows, as the reference skips them with ``continue`` (1.1.0:1246-1249).
     """
+    own = fft is None  # a processor made here lives for this call: OnInit .. OnDeinit of one chart
     fft = fft or FftProcessor()
     feed = FeedBuilder(fft_window)
     out = np.full((bars, fft_window // 2), np.nan)
-    for b in range(bars):
-        if not feed.build(cache, bars - 1 - b):
-            continue
-        detrended = feed.feed_data.copy()  # 1.1.0:1239, "windowing: none"
-        if not fft.ensure(fft_window):
-            continue
-        if not fft.run(detrended, fft_window):
-            continue
-        out[b] = fft.spectrum
+    try:
+        for b in range(bars):
+            if not feed.build(cache, bars - 1 - b):
+                continue
+            detrended = feed.feed_data.copy()  # 1.1.0:1239, "windowing: none"
+            if not fft.ensure(fft_window):
+                continue
+            if not fft.run(detrended, fft_window):
+                continue
+            out[b] = fft.spectrum
+    finally:
+        if own:
+            fft.shutdown()  # OnDeinit (1.1.0:710-716): drops this chart's reference on the session
     return out
 
 

@@ -19,3 +19,15 @@ def shard_series_slice(w0: int, nw: int, hop: int, window_len: int) -> tuple[int
     if nw <= 0:
         return w0 * hop, w0 * hop
     return w0 * hop, (w0 + nw - 1) * hop + window_len
+
+
+def shard_symbols(costs: list[float], n_shards: int, shard: int) -> list[int]:
+    """Indices of the symbols (whole per-symbol batches, C5) that `shard` owns: greedy
+    longest-first assignment to the least-loaded shard, balanced by `costs` (output bytes)."""
+    load = [0.0] * n_shards
+    owner = [0] * len(costs)
+    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        g = min(range(n_shards), key=lambda g: (load[g], g))
+        owner[i] = g
+        load[g] += costs[i]
+    return [i for i in range(len(costs)) if owner[i] == shard]

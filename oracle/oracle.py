@@ -194,3 +194,35 @@ def rel_err(p: np.ndarray, ref: np.ndarray) -> float:
     den = np.max(np.abs(ref), axis=1)
     den = np.where(den > 0, den, 1.0)
     return float(np.max(np.max(np.abs(p - ref), axis=1) / den))
+
+
+def band(n: int, min_period: float = 18.0, max_period: float = 200.0) -> tuple[int, int]:
+    """The reference's scan range [ceil(N/MaxPeriod), floor(N/MinPeriod)] clamped to N/2-1
+    (L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:539-541; InpMinPeriod 18 /
+    InpMaxPeriod 200, 1.1.0:22-23): the cycle bins the indicator actually reads."""
+    import math
+    kmin = max(0, math.ceil(n / max_period))
+    kmax = min(n // 2 - 1, math.floor(n / min_period))
+    return kmin, kmax
+
+
+def inband_err(p: np.ndarray, ref: np.ndarray, kmin: int, kmax: int) -> float:
+    """Per-window max_{k in [kmin,kmax]} |P - P_ref| / max_{k in [kmin,kmax]} P_ref, worst over
+    windows.  rel_err normalises by the whole row's maximum, which with detrend "none" is P_0
+    (~1e6 x the cycle bins at prices ~1.1): this metric holds the cycle bins to the same bar."""
+    p = np.atleast_2d(p)[:, kmin:kmax + 1]
+    ref = np.atleast_2d(ref)[:, kmin:kmax + 1]
+    den = np.max(np.abs(ref), axis=1)
+    den = np.where(den > 0, den, 1.0)
+    return float(np.max(np.max(np.abs(p - ref), axis=1) / den))
+
+
+def worst_elementwise(p: np.ndarray, ref: np.ndarray, kmin: int = 0, kmax: int | None = None) -> float:
+    """max |P_k - P_ref,k| / |P_ref,k| over the bins [kmin, kmax] (SURVEY 8c "also report worst
+    element-wise").  Reported, not a bar over the whole row: bins near zero (e.g. the Hann
+    window's nulls) carry round-off far above their own size in any fp64 FFT."""
+    p = np.atleast_2d(p)[:, kmin:None if kmax is None else kmax + 1]
+    ref = np.atleast_2d(ref)[:, kmin:None if kmax is None else kmax + 1]
+    ok = np.abs(ref) > 0
+    return float(np.max(np.abs(p - ref)[ok] / np.abs(ref)[ok])) if ok.any() else 0.0
+

@@ -1,0 +1,246 @@
+"""Parity at the benchmarked sizes: the exact kernel instantiations bench.py times, on
+full-size batches, checked against the oracle on windows sampled from the LAST
+grid-stride iterations of each launch (the library launches at most 32768
+workgroups and grid-strides: spectrum_dispatch.h kDefaultGrid), plus the in-band
+metric over the reference's cycle bins and the worst element-wise error.
+
+Also the 28-symbol C5 fetcher shape from 28 concurrent threads (one per chart,
+WaveCyclesBatchFetcher.mq5:104-133) with staggered gpu_shutdown calls.
+"""
+import ctypes as C
+import json
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+from wavespec_amd import bridge, synth
+
+pytestmark = pytest.mark.gpu
+
+GRID = 32768  # workgroups per launch (spectrum_dispatch.h kDefaultGrid)
+KALMAN = oracle.KALMAN_DEFAULTS
+METRICS = {}
+
+
+def _record(name, **kv):
+    METRICS[name] = kv
+    path = os.environ.get("WSP_PARITY_LOG")
+    if path:
+        with open(path, "w") as f:
+            json.dump(METRICS, f, indent=1)
+
+
+def _sample(nwin, per_group_windows, k=24, seed=0):
+    """Window indices: the first and last windows, a spread, and a block from the last grid-stride
+    iteration (w >= (iterations - 1) * GRID * windows-per-workgroup)."""
+    rng = np.random.default_rng(seed)
+    groups = -(-nwin // per_group_windows)
+    iters = -(-groups // GRID)
+    last0 = (iters - 1) * GRID * per_group_windows
+    tail = np.arange(last0, min(nwin, last0 + 8))
+    idx = np.unique(np.r_[0, 1, nwin - 1, nwin - 2, tail, rng.integers(last0, nwin, k // 2),
+                          rng.integers(0, nwin, k // 2)])
+    return idx, iters
+
+
+def _check_power(name, got, want, n, tol):
+    kmin, kmax = oracle.band(n)
+    full = oracle.rel_err(got, want)
+    inb = oracle.inband_err(got, want, kmin, kmax)
+    el = oracle.worst_elementwise(got, want, kmin, kmax)
+    _record(name, windows=int(got.shape[0]), rel_err=full, inband_err=inb, inband_worst_elementwise=el,
+            band=[kmin, kmax])
+    assert full <= tol, (name, full)
+    assert inb <= tol, (name, inb)
+    return el
+
+
+def test_north_star_full_grid(gpu_session):
+    """65536 x 4096 fp64 Hann, no detrend: spectrum_kernel<double,12,none,power,kWinCos> as benchmarked."""
+    torch = pytest.importorskip("torch")
+    n, w = 4096, 65536
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 11, dev)
+    d_o = torch.empty(w * n // 2, dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    assert torch.isfinite(P).all().item() and (P >= 0).all().item()
+    idx, iters = _sample(w, 1)
+    assert iters == 2 and idx.max() >= GRID
+    X = d_s.view(w, n)
+    host = X[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    got = P[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.stack([oracle.window_spectrum(x, "none", "hann") for x in host])
+    el = _check_power("north_star", got, want, n, 1e-10)
+    assert el <= 1e-8
+    # every 257th window against torch.fft with the reference's symmetric Hann
+    hann = 0.5 * (1 - torch.cos(2 * np.pi * torch.arange(n, device=dev, dtype=torch.float64) / (n - 1)))
+    F = torch.fft.rfft(X[::257] * hann, dim=1)[:, : n // 2]
+    Pt = F.real ** 2 + F.imag ** 2
+    err = ((P[::257] - Pt).abs().amax(dim=1) / Pt.abs().amax(dim=1)).max().item()
+    assert err < 1e-12
+    plan.close()
+
+
+def test_c3_kalman_f32_full_grid(gpu_session):
+    """C3: 65536 x 4096 fp32, per-window Kalman 4D + Hann (pre-pass + spectrum_kernel<float,...>)."""
+    torch = pytest.importorskip("torch")
+    n, w = 4096, 65536
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 11, dev, torch.float32)
+    d_o = torch.empty(w * n // 2, dtype=torch.float32, device=dev)
+    plan = bridge.Plan(0, n, n, w, "kalman", "hann", 0, "f32")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    assert torch.isfinite(P).all().item()
+    idx, iters = _sample(w, 1, seed=3)
+    assert idx.max() >= GRID
+    host = d_s.view(w, n)[torch.from_numpy(idx).to(dev)].double().cpu().numpy()
+    got = P[torch.from_numpy(idx).to(dev)].double().cpu().numpy()
+    want = np.stack([oracle.window_spectrum(x, "kalman", "hann", 0, kalman=KALMAN) for x in host])
+    _check_power("c3", got, want, n, 1e-5)
+    plan.close()
+
+
+def test_c4_hop1_full_grid(gpu_session):
+    """C4: 1,048,576 overlapping 2048-pt windows, hop = 1, fp64 Hann (8 GiB of spectra in HBM):
+    32 grid-stride iterations of single-wave workgroups."""
+    torch = pytest.importorskip("torch")
+    n, w = 2048, 1048576
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(w - 1 + n, 13, dev)
+    d_o = torch.empty(w * (n // 2), dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, 1, w, "none", "hann")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    idx, iters = _sample(w, 1, k=32, seed=4)
+    assert iters == 32 and idx.max() >= 31 * GRID
+    s = d_s.cpu().numpy()
+    got = P[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.stack([oracle.window_spectrum(s[i:i + n], "none", "hann") for i in idx])
+    el = _check_power("c4", got, want, n, 1e-10)
+    assert el <= 1e-8
+    assert torch.isfinite(P[-65536:]).all().item()
+    del d_o
+    plan.close()
+
+
+@pytest.mark.parametrize("output", ["topk", "topk_phase"])
+def test_ns_topk_full_grid(gpu_session, output):
+    """North star -> top-8 bins in periods [18, 200] (the benchmarked ns_topk / ns_topk_phase kernels)."""
+    torch = pytest.importorskip("torch")
+    n, w, k = 4096, 65536, 8
+    rw = 4 if output == "topk" else 6
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 11, dev)
+    d_o = torch.empty(w * rw * k, dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann", output=output)
+    plan.set_topk(k, 18.0, 200.0)
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    R = d_o.view(w, k, rw)
+    idx, _ = _sample(w, 1, seed=5)
+    host = d_s.view(w, n)[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    got = R[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    f = oracle.batch_topk if output == "topk" else oracle.batch_topk_phase
+    want = np.concatenate([f(x, n, n, "none", "hann", 0, None, k, 18.0, 200.0) for x in host])
+    spec = np.stack([oracle.window_spectrum(x, "none", "hann") for x in host])
+    kmin, kmax = oracle.band(n)
+    band_max = spec[:, kmin:kmax + 1].max(axis=1)
+    nb = 0
+    for i in range(len(idx)):
+        same = got[i, :, 0] == want[i, :, 0]
+        nb += int((~same).sum())
+        # powers of every slot within 1e-10 of the in-band maximum (rank swaps only between near-ties)
+        assert np.max(np.abs(got[i, :, 1] - want[i, :, 1])) <= 1e-10 * band_max[i], i
+        if output == "topk_phase":
+            assert np.max(np.abs(got[i, same, 4:] - want[i, same, 4:]), initial=0.0) <= 1e-8, i
+    assert nb <= 2  # a swap needs two powers equal to ~1e-10: essentially never
+    _record(f"ns_{output}", windows=len(idx), bin_mismatches=nb)
+    plan.close()
+
+
+# ------------------------------------------------------------------ C5 concurrency
+def _fetcher(sym, n, series, res, barrier_a, barrier_b, early):
+    """WaveCyclesBatchFetcher::OnTimer (WaveCyclesBatchFetcher.mq5:104-133) on the spectrum batch API:
+    gpu_init -> submit(hop 1) -> poll try_get with Sleep(5) -> gpu_free_job; then the chart's
+    OnDeinit gpu_shutdown (1.1.0:710-716), either right away (early) or after a second round."""
+    lib = bridge.lib()
+    try:
+        assert lib.gpu_init(0, 64) == bridge.OK
+
+        def one_round():
+            nwin = series.size - n + 1
+            out = np.empty((nwin, n // 2))
+            jid = C.c_int64(0)
+            st = lib.gpu_submit_spectrum_batch(bridge._dptr(series), series.size, n, 1, 0, 1, 0, 0, 0, C.byref(jid))
+            assert st == bridge.OK and jid.value > 0, st
+            ready, got = C.c_int32(0), C.c_int32(0)
+            for _ in range(12000):  # 4000 x 5 ms in the reference; longer here: 28 charts share one GPU
+                st = lib.gpu_try_get_spectrum_batch(jid.value, bridge._dptr(out), out.size, C.byref(got),
+                                                    C.byref(ready))
+                if st == bridge.OK and ready.value == 1:
+                    break
+                assert st == bridge.NOT_READY, st
+                time.sleep(0.005)
+            assert ready.value == 1 and got.value == nwin
+            assert lib.gpu_free_job(jid.value) == bridge.OK
+            return out
+
+        out1 = one_round()
+        barrier_a.wait(timeout=600)
+        if early:
+            lib.gpu_shutdown()  # this chart closes while the others still work
+            barrier_b.wait(timeout=600)
+            res[sym] = (out1, None)
+            return
+        barrier_b.wait(timeout=600)  # every early chart has shut down
+        out2 = one_round()  # the session is still open for the charts that did not shut down
+        lib.gpu_shutdown()
+        res[sym] = (out1, out2)
+    except BaseException as e:  # noqa: BLE001 -- reported by the main thread
+        res[sym] = e
+        barrier_a.abort()
+        barrier_b.abort()
+
+
+def test_c5_28_symbols_concurrent(gpu_session):
+    """C5: 28 symbols x 20000 bars, N = 512/1024/2048/4096 (7 symbols each), hop = 1, fp64 Hann,
+    from 28 threads at once; half the charts shut down while the other half keep submitting."""
+    bars, lens = 20000, (512, 1024, 2048, 4096)
+    series = [synth.random_walk(bars, 100 + s) for s in range(28)]
+    res = {}
+    ba, bb = threading.Barrier(28), threading.Barrier(28)
+    th = [threading.Thread(target=_fetcher, args=(s, lens[s // 7], series[s], res, ba, bb, s % 2 == 0))
+          for s in range(28)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    errs = {s: r for s, r in res.items() if isinstance(r, BaseException)}
+    assert not errs, errs
+    assert len(res) == 28
+    worst = 0.0
+    for s in range(28):
+        n = lens[s // 7]
+        nwin = bars - n + 1
+        idx = np.unique(np.r_[0, nwin // 2, nwin - 1, np.random.default_rng(s).integers(0, nwin, 3)])
+        want = np.stack([oracle.window_spectrum(series[s][i:i + n], "none", "hann") for i in idx])
+        for out in res[s]:
+            if out is None:
+                continue
+            assert oracle.rel_err(out[idx], want) <= 1e-10, s
+            assert oracle.inband_err(out[idx], want, *oracle.band(n)) <= 1e-10, s
+            worst = max(worst, oracle.rel_err(out[idx], want))
+    _record("c5_threads", symbols=28, rel_err=worst)
+    # the fixture's own reference still holds the session
+    s = synth.random_walk(8 * 512, seed=1)
+    assert oracle.rel_err(bridge.spectrum_batch(s, 512, 512), oracle.batch_spectrum(s, 512, 512)) <= 1e-10

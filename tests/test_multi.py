@@ -99,3 +99,46 @@ def test_shard_cover(W, G):
         w0, nw = sharding.shard_windows(W, G, g)
         seen.extend(range(w0, w0 + nw))
     assert seen == list(range(W))
+
+
+def _bench_line(*args, env=None):
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, timeout=300,
+                       env=env)
+    return r, [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_gpus2_spawns_ranks_and_shards_c4():
+    """`bench.py --gpus 2` outside torchrun starts 2 ranks (gloo rendezvous on 127.0.0.1) that split C4's
+    1,048,576 hop=1 windows into contiguous ranges, each reading its slice plus the N - hop halo."""
+    r, lines = _bench_line("--gpus", "2", "--config", "c4", "--scaling", "strong", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = lines
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    s0, s1 = line["shards"]
+    n, hop, W = 2048, 1, 1048576
+    assert s0["w0"] == 0 and s1["w0"] == s0["windows"] and s0["windows"] + s1["windows"] == W
+    for sh in (s0, s1):
+        a, b = sh["series"]
+        assert a == sh["w0"] * hop and b == (sh["w0"] + sh["windows"] - 1) * hop + n
+    assert s0["series"][1] - s1["series"][0] == n - hop  # the halo both ranks read
+
+
+def test_bench_c5_strong_symbols_partition():
+    r, lines = _bench_line("--gpus", "2", "--config", "c5", "--scaling", "strong", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = lines
+    syms = sorted(s for sh in line["shards"] for s in sh["symbols"])
+    assert syms == list(range(28))
+    assert sum(sh["windows"] for sh in line["shards"]) == 506268
+    lens = (512, 1024, 2048, 4096)
+    out_bytes = [sum((20000 - lens[s // 7] + 1) * lens[s // 7] // 2 for s in sh["symbols"]) for sh in line["shards"]]
+    assert max(out_bytes) / min(out_bytes) < 1.05  # balanced by the bytes each rank writes
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r, lines = _bench_line("--gpus", "2", "--plan-only", env=env)
+    assert r.returncode != 0 and not lines and "WORLD_SIZE=1" in r.stderr
