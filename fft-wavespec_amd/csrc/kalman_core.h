@@ -72,58 +72,258 @@ inline int kalman_flags(const KP &kp) {
     return (kp.adapt > 0.0 ? kKfAdapt : 0) | (kp.clip > 0.0 ? kKfClip : 0) | (kp.ema > 0.0 ? kKfEma : 0);
 }
 
-// WPW windows per wave (64, or 32 so that two waves share a SIMD and hide each
-// other's dependency stalls when the batch has only one window per lane).
-// PKUP (fp32 filter): the update in normalised form, g = P_0./sqrt(S), with
-// the state and covariance updates as packed pairs (v_pk_fma_f32), about 10
-// fewer instructions per step (0.743 -> 0.678 ms at C3).
+// Filter state of one lane (centred on the window's first sample x0) and the
+// step constants.
+template <typename K> struct KState {
+    K pos, vel, acc, jerk;
+    K p00, p01, p02, p03, p11, p12, p13, p22, p23, p33;
+    K ema_prev;
+    bool ema_ready;
+};
+template <typename K> struct KConst {
+    K Qp, Qv, Qa, Qj, R, gQp, gQv, gQa, gQj, adapt, clip, ema_a;
+    bool use_adapt, use_clip, use_ema;
+};
+
+template <typename K, int FL> __device__ __forceinline__ KConst<K> kconst(const KP &kp) {
+    KConst<K> c;
+    const K q_scale = (K)fmax(0.05, kp.follow);
+    c.Qp = (K)fmax(1e-9, kp.qp * (double)q_scale);
+    c.Qv = (K)fmax(1e-9, kp.qv * (double)q_scale);
+    c.Qa = (K)fmax(1e-9, kp.qa * (double)q_scale);
+    c.Qj = (K)fmax(1e-9, kp.qj * (double)q_scale);
+    c.R = (K)fmax(1e-9, kp.r);
+    c.adapt = (K)kp.adapt;
+    c.clip = (K)kp.clip;
+    c.gQp = c.adapt * c.Qp;
+    c.gQv = c.adapt * c.Qv;
+    c.gQa = c.adapt * c.Qa;
+    c.gQj = c.adapt * c.Qj;
+    c.use_adapt = FL >= 0 ? (FL & kKfAdapt) != 0 : kp.adapt > 0.0;
+    c.use_clip = FL >= 0 ? (FL & kKfClip) != 0 : kp.clip > 0.0;
+    c.use_ema = FL >= 0 ? (FL & kKfEma) != 0 : kp.ema > 0.0;
+    c.ema_a = c.use_ema ? (K)(2.0 / (kp.ema + 1.0)) : K(0);
+    return c;
+}
+
+// ResetKalmanState(first_meas) :2015-2029, centred: pos = first_meas - x0
+template <typename K> __device__ __forceinline__ void kreset(KState<K> &s, const KP &kp, K pos0) {
+    s.pos = pos0;
+    s.vel = (K)kp.iv;
+    s.acc = (K)kp.ia;
+    s.jerk = (K)kp.ij;
+    s.p00 = (K)fmax(1e-9, kp.vp);
+    s.p11 = (K)fmax(1e-9, kp.vv);
+    s.p22 = (K)fmax(1e-9, kp.va);
+    s.p33 = (K)fmax(1e-9, kp.vj);
+    s.p01 = s.p02 = s.p03 = s.p12 = s.p13 = s.p23 = K(0);
+    s.ema_prev = K(0);
+    s.ema_ready = false;
+}
+
+// StepKalman4D :2031-2125 on the symmetric covariance; returns the trend.
 // TWO: predicted covariance through A = F P in two stages (32 instead of 41
 // add/fma; F is the constant-jerk transition, P symmetric) instead of the
-// reference's expanded sums -- same values, including the reference's
-// extra terms in P11.
+// reference's expanded sums -- same values, including the reference's extra
+// terms in P11.  PK (fp32 filter): the update in normalised form, g = P_0./sqrt(S),
+// with the state and covariance updates as packed pairs (v_pk_fma_f32), about 10
+// fewer instructions per step (0.743 -> 0.678 ms at C3).
+template <typename K, bool TWO, bool PKUP>
+__device__ __forceinline__ K kstep(KState<K> &st, const KConst<K> &c, K z) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    constexpr bool PK = TWO && std::is_same<K, float>::value && PKUP;
+    const K pos = st.pos, vel = st.vel, acc = st.acc, jerk = st.jerk;
+    const K p00 = st.p00, p01 = st.p01, p02 = st.p02, p03 = st.p03, p11 = st.p11, p12 = st.p12, p13 = st.p13,
+            p22 = st.p22, p23 = st.p23, p33 = st.p33;
+    const K x0p = pos + vel + K(0.5) * acc + K(1.0 / 6.0) * jerk;
+    const K x1p = vel + acc + K(0.5) * jerk;
+    const K x2p = acc + jerk;
+    const K x3p = jerk;
+    K P00p, P01p, P02p, P03p, P11p, P12p, P13p, P22p, P23p, P33p;
+    if constexpr (TWO) {
+        // A = F P (rows of F: [1 1 1/2 1/6] [0 1 1 1/2] [0 0 1 1] [0 0 0 1]); only the
+        // entries F A^T needs on and above the diagonal
+        const K a00 = p00 + p01 + K(0.5) * p02 + K(1.0 / 6.0) * p03;
+        const K a01 = p01 + p11 + K(0.5) * p12 + K(1.0 / 6.0) * p13;
+        const K a02 = p02 + p12 + K(0.5) * p22 + K(1.0 / 6.0) * p23;
+        const K a03 = p03 + p13 + K(0.5) * p23 + K(1.0 / 6.0) * p33;
+        const K a11 = p11 + p12 + K(0.5) * p13;
+        const K a12 = p12 + p22 + K(0.5) * p23;
+        const K a13 = p13 + p23 + K(0.5) * p33;
+        const K a22 = p22 + p23;
+        const K a23 = p23 + p33;
+        // Pp = A F^T
+        P00p = a00 + a01 + K(0.5) * a02 + K(1.0 / 6.0) * a03 + c.Qp;
+        P01p = a01 + a02 + K(0.5) * a03;
+        P02p = a02 + a03;
+        P03p = a03;
+        // the reference's P11 prediction (:2052) is not (F P F^T)_11: it adds
+        // p12 + p22 + (p13 + p23)/2 = a12 + p13/2, kept for parity
+        P11p = a11 + K(2) * a12 + K(0.5) * (a13 + p13) + c.Qv;
+        P12p = a12 + a13;
+        P13p = a13;
+        P22p = a22 + a23 + c.Qa;
+        P23p = a23;
+        P33p = p33 + c.Qj;
+    } else {
+        P00p = p00 + K(2) * p01 + p02 + K(1.0 / 3.0) * p03 + p11 + p12 + K(1.0 / 3.0) * p13 + K(0.25) * p22 +
+               K(1.0 / 6.0) * p23 + K(1.0 / 36.0) * p33 + c.Qp;
+        P01p = p01 + p02 + K(0.5) * p03 + p11 + K(1.5) * p12 + K(2.0 / 3.0) * p13 + K(0.5) * p22 +
+               K(5.0 / 12.0) * p23 + K(1.0 / 12.0) * p33;
+        P02p = p02 + p03 + p12 + p13 + K(0.5) * p22 + K(2.0 / 3.0) * p23 + K(1.0 / 6.0) * p33;
+        P03p = p03 + p13 + K(0.5) * p23 + K(1.0 / 6.0) * p33;
+        P11p = p11 + K(3) * p12 + K(1.5) * p13 + K(2) * p22 + K(1.5) * p23 + K(0.25) * p33 + c.Qv;
+        P12p = p12 + p13 + p22 + K(1.5) * p23 + K(0.5) * p33;
+        P13p = p13 + p23 + K(0.5) * p33;
+        P22p = p22 + K(2) * p23 + p33 + c.Qa;
+        P23p = p23 + p33;
+        P33p = p33 + c.Qj;
+    }
+
+    K y = z - x0p;
+    K S = P00p + c.R;
+    if (c.use_adapt) {
+        if constexpr (TWO) {  // boost - 1 = min(5,|y|/sigma) g, g folded into the Q terms
+            const K k = fmin(K(5), fabs(y) * krsqrt(S));
+            P00p += k * c.gQp;
+            P11p += k * c.gQv;
+            P22p += k * c.gQa;
+            P33p += k * c.gQj;
+        } else {
+            const K k = fmin(K(5), fabs(y) * krsqrt(S)) * c.adapt;
+            P00p += k * c.Qp;
+            P11p += k * c.Qv;
+            P22p += k * c.Qa;
+            P33p += k * c.Qj;
+        }
+        S = P00p + c.R;
+    }
+    const K rs = krsqrt(S);
+    if constexpr (PK) {
+        // Normalised form: g_i = P_0i / sqrt(S), y_n = y / sqrt(S) clipped to +-clip, so
+        // K_i y = g_i y_n and K_i P_0j = g_i g_j.  Pairs (g0, g1), (g2, g3) and the
+        // symmetric update as four packed fma (v_pk_fma_f32: one issue for two lanes' worth).
+        K yn = y * rs;
+        if (c.use_clip) yn = kclamp(yn, c.clip);
+        const f2v pa = {P00p, P01p}, pb = {P02p, P03p};
+        const f2v g01 = pa * rs, g23 = pb * rs;
+        const f2v s01 = f2v{x0p, x1p} + g01 * yn, s23 = f2v{x2p, x3p} + g23 * yn;
+        st.pos = s01.x;
+        st.vel = s01.y;
+        st.acc = s23.x;
+        st.jerk = s23.y;
+        const f2v q0 = pa - g01 * g01.x, q1 = pb - g23 * g01.x;
+        const f2v q2 = f2v{P12p, P13p} - g23 * g01.y, q3 = f2v{P22p, P23p} - g23 * g23.x;
+        st.p00 = fmax(K(1e-12), q0.x);
+        st.p01 = q0.y;
+        st.p02 = q1.x;
+        st.p03 = q1.y;
+        st.p11 = fmax(K(1e-12), P11p - g01.y * g01.y);
+        st.p12 = q2.x;
+        st.p13 = q2.y;
+        st.p22 = fmax(K(1e-12), q3.x);
+        st.p23 = q3.y;
+        st.p33 = fmax(K(1e-12), P33p - g23.y * g23.y);
+    } else {
+        if (c.use_clip) y = kclamp(y, c.clip * (S * rs));  // clip * sqrt(S)
+        const K inv = rs * rs;  // 1/S
+        const K K0 = P00p * inv, K1 = P01p * inv, K2 = P02p * inv, K3 = P03p * inv;
+        st.pos = x0p + K0 * y;
+        st.vel = x1p + K1 * y;
+        st.acc = x2p + K2 * y;
+        st.jerk = x3p + K3 * y;
+        // P_ij <- P_ij - K_i P_0j (symmetric), diagonal floors 1e-12
+        st.p00 = fmax(K(1e-12), P00p - K0 * P00p);
+        st.p01 = P01p - K1 * P00p;
+        st.p02 = P02p - K2 * P00p;
+        st.p03 = P03p - K3 * P00p;
+        st.p11 = fmax(K(1e-12), P11p - K1 * P01p);
+        st.p12 = P12p - K2 * P01p;
+        st.p13 = P13p - K3 * P01p;
+        st.p22 = fmax(K(1e-12), P22p - K2 * P02p);
+        st.p23 = P23p - K3 * P02p;
+        st.p33 = fmax(K(1e-12), P33p - K3 * P03p);
+    }
+
+    K trend = st.pos;
+    if (c.use_ema) {  // :2117-2123
+        if (!st.ema_ready) {
+            st.ema_prev = trend;
+            st.ema_ready = true;
+        }
+        st.ema_prev = c.ema_a * trend + (K(1) - c.ema_a) * st.ema_prev;
+        trend = st.ema_prev;
+    }
+    return trend;
+}
+
+// Segments of one window's filter.  SEG = 1: one lane runs the window's N steps.
+// SEG = 2 (parallel in time): lane pair (l, l + 32) splits window l: the first
+// lane runs samples [0, L0) from the reset as usual, the second lane starts
+// cold -- ResetKalmanState at sample L0 - WU -- runs WU warm-up steps without
+// output, then samples [L0, N), L0 = (N + WU)/2 so that both run L0 steps.  The
+// filter forgets its initial state: a cold start contracts onto the sequential
+// filter's trajectory (oracle.numpy_kalman_trend: 4e-16 after 256 steps on the
+// C3 data) until rounding makes the two states identical, after which the
+// deterministic recurrence keeps them identical.  The result is VERIFIED, not
+// assumed: at the end the first lane's state after sample L0 - 1 is compared
+// BIT FOR BIT with the second lane's state after its warm-up (all 14 values,
+// + the EMA state when enabled); if any differs, the second lanes of the wave
+// re-run [L0, N) from the first lanes' state.  Either way every output is
+// bit-identical to the one-lane filter's.  Twice the lanes per window: at C3's
+// 65536 windows the filter gets two waves per SIMD instead of one lone wave,
+// which issues VALU every 2 instead of every 4 cycles (MI355X_MICROARCH.md,
+// vector issue cost), at (N + WU)/2N of the steps per lane.
+constexpr int kSegWarm = 512;
+template <typename K> __device__ __forceinline__ bool kclose(K a, K b) {
+    return __builtin_bit_cast(typename std::conditional<sizeof(K) == 4, unsigned, unsigned long long>::type, a) ==
+           __builtin_bit_cast(typename std::conditional<sizeof(K) == 4, unsigned, unsigned long long>::type, b);
+}
+template <typename K> __device__ __forceinline__ K kxor32(K v) {  // value of lane l ^ 32
+    if constexpr (sizeof(K) == 4) {
+        return __builtin_bit_cast(K, __shfl_xor(__builtin_bit_cast(int, v), 32, 64));
+    } else {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        const int lo = __shfl_xor((int)(unsigned)u, 32, 64), hi = __shfl_xor((int)(unsigned)(u >> 32), 32, 64);
+        return __builtin_bit_cast(K, (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32));
+    }
+}
+
+// WPW windows per wave (64, or 32 so that two waves share a SIMD and hide each
+// other's dependency stalls when the batch has only one window per lane).
 // WAVES: independent waves per workgroup (each its own WPW windows and LDS
 // tile).  With WAVES = 4 and an LDS reservation that admits one workgroup per
 // CU, a batch of at most 64 windows per SIMD runs exactly one wave on every
 // SIMD; single-wave workgroups may be stacked two to a SIMD by the dispatcher
 // while other SIMDs idle (measured: 0.76 ms back-to-back, 1.1 ms after a
-// spectrum launch at C3).
+// spectrum launch at C3).  SEG = 2 requires WPW = 32 (lane pairs l, l + 32).
+// `fallbacks` (tools only, may be null): waves that re-ran their second segments.
 template <typename T, typename K, int J, int WPW, int UNROLL = 2, int FL = kKfRuntime, bool TWO = false, int WAVES = 1,
-          bool PKUP = false>
+          bool PKUP = false, int SEG = 1, int WU = kSegWarm>
 __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__restrict__ series, T *__restrict__ dout,
-                                                                    int64_t hop, int64_t n_windows, int n, KP kp) {
-    __shared__ T tiles[WAVES][WPW * (J + 1)];  // per wave: [window row][step], +1 pad: conflict-free row walks
+                                                                    int64_t hop, int64_t n_windows, int n, KP kp,
+                                                                    unsigned *fallbacks = nullptr, double *dbg = nullptr) {
+    static_assert(SEG == 1 || (SEG == 2 && WPW == 32), "two segments pair lanes l and l + 32");
+    __shared__ T tiles[WAVES][64 * (J + 1)];  // per wave: [row][step], +1 pad: conflict-free row walks
     // wave index through readfirstlane: provably uniform, so the descriptors stay scalar
     const int l = threadIdx.x % 64, wv = WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / 64) : 0;
     T *tile = tiles[wv];
     const int64_t w0 = ((int64_t)blockIdx.x * WAVES + wv) * WPW;
-    const bool lane_on = l < WPW;
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    // packed-pair update for the fp32 filter (fp64 has no packed fma)
-    constexpr bool PK = TWO && std::is_same<K, float>::value && PKUP;
+    // rows of the tile: SEG = 1, row r = window r; SEG = 2, row r = segment r / 32 of window r % 32
+    constexpr int ROWS = 64;
+    const bool lane_on = SEG == 2 || l < WPW;
+    const KConst<K> kc = kconst<K, FL>(kp);
+    // segment geometry (SEG = 2): both lanes run L0 steps; the second lane's samples start at L0 - WU
+    const int L0 = SEG == 2 ? (n + WU) / 2 : n;
+    const int seg_off = L0 - WU;  // series offset of the second segment's first (warm-up) sample
+    const int nchunks = L0 / J;
+    constexpr int WUC = WU / J;  // warm-up chunks of the second segment
+    static_assert(WU % 32 == 0, "whole tiles of warm-up");
 
-    const K q_scale = (K)fmax(0.05, kp.follow);
-    const K Qp = (K)fmax(1e-9, kp.qp * (double)q_scale), Qv = (K)fmax(1e-9, kp.qv * (double)q_scale);
-    const K Qa = (K)fmax(1e-9, kp.qa * (double)q_scale), Qj = (K)fmax(1e-9, kp.qj * (double)q_scale);
-    const K R = (K)fmax(1e-9, kp.r);
-    const K adapt = (K)kp.adapt, clip = (K)kp.clip;
-    const K gQp = adapt * Qp, gQv = adapt * Qv, gQa = adapt * Qa, gQj = adapt * Qj;
-    const bool use_adapt = FL >= 0 ? (FL & kKfAdapt) != 0 : kp.adapt > 0.0;
-    const bool use_clip = FL >= 0 ? (FL & kKfClip) != 0 : kp.clip > 0.0;
-    const bool use_ema = FL >= 0 ? (FL & kKfEma) != 0 : kp.ema > 0.0;
-    const K ema_a = use_ema ? (K)(2.0 / (kp.ema + 1.0)) : K(0);
-
-    // ResetKalmanState(first_meas) :2015-2029, centred: pos' = 0
-    K pos = 0, vel = (K)kp.iv, acc = (K)kp.ia, jerk = (K)kp.ij;
-    K p00 = (K)fmax(1e-9, kp.vp), p11 = (K)fmax(1e-9, kp.vv), p22 = (K)fmax(1e-9, kp.va), p33 = (K)fmax(1e-9, kp.vj);
-    K p01 = 0, p02 = 0, p03 = 0, p12 = 0, p13 = 0, p23 = 0;
-    bool ema_ready = false;
-    K ema_prev = 0;
-    T x0 = 0;
-
-    // tile rows are windows w0 .. w0+WPW-1; row r, step j of chunk c = series[(w0+r)*hop + c*J + j].
-    // One wave instruction moves RPI rows of J contiguous samples (coalesced).  Offsets are
+    // tile rows are windows w0 .. w0+WPW-1 (x SEG); row r, step j of chunk c = series[(w0+wr)*hop + sr*seg_off +
+    // c*J + j].  One wave instruction moves RPI rows of J contiguous samples (coalesced).  Offsets are
     // 32-bit: the host guarantees WPW*hop and WPW*n elements fit in 2 GiB.
-    constexpr int RPI = 64 / J, NI = WPW / RPI;
+    constexpr int RPI = 64 / J, NI = ROWS / RPI, NIS = NI / SEG;  // NIS instructions per segment
     const int lrow = l / J, lcol = l % J;
     // rows <= 0: a wave of the last workgroup past the batch end; its descriptors are
     // empty (loads read 0, stores are dropped) and it keeps step with the barriers
@@ -132,159 +332,95 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
     const auto rout = kbuf(dout + w0 * (int64_t)n, (uint32_t)(rows * n * (int64_t)sizeof(T)));
     const uint32_t vin = (uint32_t)((lrow * hop + lcol) * (int64_t)sizeof(T));
     const uint32_t vout = (uint32_t)((lrow * n + lcol) * (int)sizeof(T));
+    // per-instruction row offsets (uniform): instruction i covers rows i*RPI + lrow
+    auto in_row = [&](int i) { return (uint32_t)((((i % NIS) * RPI) * hop + (i / NIS) * (int64_t)seg_off) * (int64_t)sizeof(T)); };
+    auto out_row = [&](int i) { return (uint32_t)((((i % NIS) * RPI) * (int64_t)n + (i / NIS) * (int64_t)seg_off) * (int64_t)sizeof(T)); };
     T reg[NI];
-    const int nchunks = n / J;
     auto issue = [&](int c) {
         const uint32_t vc = vin + (uint32_t)(c * J * (int)sizeof(T));
 #pragma unroll
-        for (int i = 0; i < NI; ++i) reg[i] = kload(rin, vc + (uint32_t)(i * RPI * hop * (int64_t)sizeof(T)), 0u, T());
+        for (int i = 0; i < NI; ++i) reg[i] = kload(rin, vc + in_row(i), 0u, T());
     };
-    issue(0);
-    for (int c = 0; c < nchunks; ++c) {
+
+    KState<K> st;
+    T x0 = 0;
+    const int lr = lane_on ? l : 0;
+    // filters chunks [c0, c1) of every lane; stores the rows of segment 0 for c >= s0 and of segment 1
+    // for c >= s1 (SEG = 2: its warm-up chunks produce no output)
+    auto run = [&](int c0, int c1, int s0, int s1, bool save_warm, KState<K> &warm) {
+        issue(c0);
+        for (int c = c0; c < c1; ++c) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) tile[(i * RPI + lrow) * (J + 1) + lcol] = reg[i];
-        __syncthreads();
-        if (c + 1 < nchunks) issue(c + 1);  // next tile in flight while the lanes filter this one
-        const int lr = lane_on ? l : 0;
-        if (c == 0) x0 = tile[lr * (J + 1)];
-        T zrow[J];  // this window's J samples in registers: no LDS latency inside the recurrence
+            for (int i = 0; i < NI; ++i) tile[(i * RPI + lrow) * (J + 1) + lcol] = reg[i];
+            __syncthreads();
+            if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
+            if (c == 0) {
+                x0 = tile[(SEG == 2 ? lr % 32 : lr) * (J + 1)];  // the window's first sample
+                const T first = tile[lr * (J + 1)];             // this lane's first sample
+                kreset<K>(st, kp, (K)(first - x0));
+            }
+            T zrow[J];  // this row's J samples in registers: no LDS latency inside the recurrence
 #pragma unroll
-        for (int j = 0; j < J; ++j) zrow[j] = tile[lr * (J + 1) + j];
+            for (int j = 0; j < J; ++j) zrow[j] = tile[lr * (J + 1) + j];
 #pragma unroll UNROLL
-        for (int j = 0; j < J; ++j) {
-            const T zt = zrow[j];
-            const K z = (K)(zt - x0);  // exact for prices within 2x of x0 (Sterbenz)
-            // StepKalman4D :2031-2125 on the symmetric covariance
-            const K x0p = pos + vel + K(0.5) * acc + K(1.0 / 6.0) * jerk;
-            const K x1p = vel + acc + K(0.5) * jerk;
-            const K x2p = acc + jerk;
-            const K x3p = jerk;
-            K P00p, P01p, P02p, P03p, P11p, P12p, P13p, P22p, P23p, P33p;
-            if constexpr (TWO) {
-                // A = F P (rows of F: [1 1 1/2 1/6] [0 1 1 1/2] [0 0 1 1] [0 0 0 1]); only the
-                // entries F A^T needs on and above the diagonal
-                const K a00 = p00 + p01 + K(0.5) * p02 + K(1.0 / 6.0) * p03;
-                const K a01 = p01 + p11 + K(0.5) * p12 + K(1.0 / 6.0) * p13;
-                const K a02 = p02 + p12 + K(0.5) * p22 + K(1.0 / 6.0) * p23;
-                const K a03 = p03 + p13 + K(0.5) * p23 + K(1.0 / 6.0) * p33;
-                const K a11 = p11 + p12 + K(0.5) * p13;
-                const K a12 = p12 + p22 + K(0.5) * p23;
-                const K a13 = p13 + p23 + K(0.5) * p33;
-                const K a22 = p22 + p23;
-                const K a23 = p23 + p33;
-                // Pp = A F^T
-                P00p = a00 + a01 + K(0.5) * a02 + K(1.0 / 6.0) * a03 + Qp;
-                P01p = a01 + a02 + K(0.5) * a03;
-                P02p = a02 + a03;
-                P03p = a03;
-                // the reference's P11 prediction (:2052) is not (F P F^T)_11: it adds
-                // p12 + p22 + (p13 + p23)/2 = a12 + p13/2, kept for parity
-                P11p = a11 + K(2) * a12 + K(0.5) * (a13 + p13) + Qv;
-                P12p = a12 + a13;
-                P13p = a13;
-                P22p = a22 + a23 + Qa;
-                P23p = a23;
-                P33p = p33 + Qj;
-            } else {
-                P00p = p00 + K(2) * p01 + p02 + K(1.0 / 3.0) * p03 + p11 + p12 + K(1.0 / 3.0) * p13 +
-                       K(0.25) * p22 + K(1.0 / 6.0) * p23 + K(1.0 / 36.0) * p33 + Qp;
-                P01p = p01 + p02 + K(0.5) * p03 + p11 + K(1.5) * p12 + K(2.0 / 3.0) * p13 + K(0.5) * p22 +
-                       K(5.0 / 12.0) * p23 + K(1.0 / 12.0) * p33;
-                P02p = p02 + p03 + p12 + p13 + K(0.5) * p22 + K(2.0 / 3.0) * p23 + K(1.0 / 6.0) * p33;
-                P03p = p03 + p13 + K(0.5) * p23 + K(1.0 / 6.0) * p33;
-                P11p = p11 + K(3) * p12 + K(1.5) * p13 + K(2) * p22 + K(1.5) * p23 + K(0.25) * p33 + Qv;
-                P12p = p12 + p13 + p22 + K(1.5) * p23 + K(0.5) * p33;
-                P13p = p13 + p23 + K(0.5) * p33;
-                P22p = p22 + K(2) * p23 + p33 + Qa;
-                P23p = p23 + p33;
-                P33p = p33 + Qj;
+            for (int j = 0; j < J; ++j) {
+                const K z = (K)(zrow[j] - x0);  // exact for prices within 2x of x0 (Sterbenz)
+                const K trend = kstep<K, TWO, PKUP>(st, kc, z);
+                zrow[j] = T(z - trend);
             }
-
-            K y = z - x0p;
-            K S = P00p + R;
-            if (use_adapt) {
-                if constexpr (TWO) {  // boost - 1 = min(5,|y|/sigma) g, g folded into the Q terms
-                    const K k = fmin(K(5), fabs(y) * krsqrt(S));
-                    P00p += k * gQp;
-                    P11p += k * gQv;
-                    P22p += k * gQa;
-                    P33p += k * gQj;
-                } else {
-                    const K k = fmin(K(5), fabs(y) * krsqrt(S)) * adapt;
-                    P00p += k * Qp;
-                    P11p += k * Qv;
-                    P22p += k * Qa;
-                    P33p += k * Qj;
-                }
-                S = P00p + R;
+            if constexpr (SEG == 2) {
+                if (save_warm && c == WUC - 1) warm = st;  // the second lanes' state after sample L0 - 1
             }
-            const K rs = krsqrt(S);
-            if constexpr (PK) {
-                // Normalised form: g_i = P_0i / sqrt(S), y_n = y / sqrt(S) clipped to +-clip, so
-                // K_i y = g_i y_n and K_i P_0j = g_i g_j.  Pairs (g0, g1), (g2, g3) and the
-                // symmetric update as four packed fma (v_pk_fma_f32: one issue for two lanes' worth).
-                K yn = y * rs;
-                if (use_clip) yn = kclamp(yn, clip);
-                const f2v pa = {P00p, P01p}, pb = {P02p, P03p};
-                const f2v g01 = pa * rs, g23 = pb * rs;
-                const f2v s01 = f2v{x0p, x1p} + g01 * yn, s23 = f2v{x2p, x3p} + g23 * yn;
-                pos = s01.x;
-                vel = s01.y;
-                acc = s23.x;
-                jerk = s23.y;
-                const f2v q0 = pa - g01 * g01.x, q1 = pb - g23 * g01.x;
-                const f2v q2 = f2v{P12p, P13p} - g23 * g01.y, q3 = f2v{P22p, P23p} - g23 * g23.x;
-                p00 = fmax(K(1e-12), q0.x);
-                p01 = q0.y;
-                p02 = q1.x;
-                p03 = q1.y;
-                p11 = fmax(K(1e-12), P11p - g01.y * g01.y);
-                p12 = q2.x;
-                p13 = q2.y;
-                p22 = fmax(K(1e-12), q3.x);
-                p23 = q3.y;
-                p33 = fmax(K(1e-12), P33p - g23.y * g23.y);
-            } else {
-                if (use_clip) y = kclamp(y, clip * (S * rs));  // clip * sqrt(S)
-                const K inv = rs * rs;  // 1/S
-                const K K0 = P00p * inv, K1 = P01p * inv, K2 = P02p * inv, K3 = P03p * inv;
-                pos = x0p + K0 * y;
-                vel = x1p + K1 * y;
-                acc = x2p + K2 * y;
-                jerk = x3p + K3 * y;
-                // P_ij <- P_ij - K_i P_0j (symmetric), diagonal floors 1e-12
-                p00 = fmax(K(1e-12), P00p - K0 * P00p);
-                p01 = P01p - K1 * P00p;
-                p02 = P02p - K2 * P00p;
-                p03 = P03p - K3 * P00p;
-                p11 = fmax(K(1e-12), P11p - K1 * P01p);
-                p12 = P12p - K2 * P01p;
-                p13 = P13p - K3 * P01p;
-                p22 = fmax(K(1e-12), P22p - K2 * P02p);
-                p23 = P23p - K3 * P02p;
-                p33 = fmax(K(1e-12), P33p - K3 * P03p);
-            }
-
-            K trend = pos;
-            if (use_ema) {  // :2117-2123
-                if (!ema_ready) {
-                    ema_prev = trend;
-                    ema_ready = true;
-                }
-                ema_prev = ema_a * trend + (K(1) - ema_a) * ema_prev;
-                trend = ema_prev;
-            }
-            zrow[j] = T(z - trend);
-        }
-        if (lane_on) {
+            if (lane_on) {
 #pragma unroll
-            for (int j = 0; j < J; ++j) tile[l * (J + 1) + j] = zrow[j];
-        }
-        __syncthreads();
+                for (int j = 0; j < J; ++j) tile[l * (J + 1) + j] = zrow[j];
+            }
+            __syncthreads();
+            const uint32_t vc = vout + (uint32_t)(c * J * (int)sizeof(T));
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
-            kstore(tile[(i * RPI + lrow) * (J + 1) + lcol], rout, vout + (uint32_t)((i * RPI * n + c * J) * (int)sizeof(T)), 0u);
-        __syncthreads();
+            for (int i = 0; i < NI; ++i)
+                if (c >= (i / NIS == 0 ? s0 : s1))
+                    kstore(tile[(i * RPI + lrow) * (J + 1) + lcol], rout, vc + out_row(i), 0u);
+            __syncthreads();
+        }
+    };
+    KState<K> warm;
+    if constexpr (SEG == 1) {
+        run(0, nchunks, 0, 0, false, warm);
+    } else {
+        run(0, nchunks, 0, WUC, true, warm);
+        // verify: the first lane's exact state after sample L0 - 1 against the second lane's warm-up state
+        KState<K> ex;
+        ex.pos = kxor32(st.pos), ex.vel = kxor32(st.vel), ex.acc = kxor32(st.acc), ex.jerk = kxor32(st.jerk);
+        ex.p00 = kxor32(st.p00), ex.p01 = kxor32(st.p01), ex.p02 = kxor32(st.p02), ex.p03 = kxor32(st.p03);
+        ex.p11 = kxor32(st.p11), ex.p12 = kxor32(st.p12), ex.p13 = kxor32(st.p13), ex.p22 = kxor32(st.p22);
+        ex.p23 = kxor32(st.p23), ex.p33 = kxor32(st.p33), ex.ema_prev = kxor32(st.ema_prev);
+        ex.ema_ready = __shfl_xor((int)st.ema_ready, 32, 64) != 0;
+        bool ok = kclose(ex.pos, warm.pos) && kclose(ex.vel, warm.vel) && kclose(ex.acc, warm.acc) &&
+                  kclose(ex.jerk, warm.jerk) && kclose(ex.p00, warm.p00) && kclose(ex.p01, warm.p01) &&
+                  kclose(ex.p02, warm.p02) && kclose(ex.p03, warm.p03) && kclose(ex.p11, warm.p11) &&
+                  kclose(ex.p12, warm.p12) && kclose(ex.p13, warm.p13) && kclose(ex.p22, warm.p22) &&
+                  kclose(ex.p23, warm.p23) && kclose(ex.p33, warm.p33);
+        if (kc.use_ema) ok = ok && ex.ema_ready == warm.ema_ready && kclose(ex.ema_prev, warm.ema_prev);
+        if (l < 32) ok = true;  // only the second lanes' outputs depend on the check
+        if (dbg && l >= 32 && w0 + (l - 32) < n_windows) {  // tools: exact state and warm-up state per window
+            double *q = dbg + (w0 + l - 32) * 28;
+            const K e[14] = {ex.pos, ex.vel, ex.acc, ex.jerk, ex.p00, ex.p01, ex.p02, ex.p03, ex.p11, ex.p12, ex.p13, ex.p22, ex.p23, ex.p33};
+            const K wv2[14] = {warm.pos, warm.vel, warm.acc, warm.jerk, warm.p00, warm.p01, warm.p02, warm.p03, warm.p11, warm.p12, warm.p13, warm.p22, warm.p23, warm.p33};
+            for (int k = 0; k < 14; ++k) {
+                q[k] = (double)e[k];
+                q[14 + k] = (double)wv2[k];
+            }
+        }
+        if (__ballot(!ok)) {  // wave-uniform: the second lanes re-run [L0, N) from the exact state
+            if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
+            const T x0keep = x0;
+            st = ex;
+            // chunks WUC .. nchunks-1 of the second segment; the first lanes recompute their own last
+            // chunks' values, which are not stored (s0 past the end)
+            run(WUC, nchunks, nchunks, WUC, false, warm);
+            x0 = x0keep;
+        }
     }
 }
 

@@ -21,17 +21,20 @@ int cu_count() {
 // use single-wave workgroups so that two waves can share a SIMD.
 template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
     constexpr int J = sizeof(T) == 4 ? 32 : 16;  // steps per tile; divides every window length >= 32
-    const bool spread = L.variant == 0 && L.n_windows <= 4LL * 64 * cu_count();
+    constexpr size_t kStatic = 4 * 64 * (J + 1) * sizeof(T);
+    const int cus = cu_count();
+    const bool spread = L.variant != 1 && L.n_windows <= 4LL * 64 * cus;
     if (spread) {
-        constexpr size_t kStatic = 4 * 64 * (J + 1) * sizeof(T);
         const size_t reserve = 84 * 1024 - kStatic;  // > half of the CU's 160 KiB: one workgroup per CU
         const unsigned grid = (unsigned)((L.n_windows + 255) / 256);
         hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 4, true>), dim3(grid), dim3(256), reserve, stream,
-                           static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp);
+                           static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp,
+                           (unsigned *)nullptr);
     } else {
         const unsigned grid = (unsigned)((L.n_windows + 63) / 64);
         hipLaunchKernelGGL((kalman_detrend_kernel<T, T, J, 64, J, FL, true, 1, true>), dim3(grid), dim3(64), 0, stream,
-                           static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp);
+                           static_cast<const T *>(L.series), static_cast<T *>(L.detrended), L.hop, L.n_windows, L.n, kp,
+                           (unsigned *)nullptr);
     }
     return hipGetLastError();
 }

@@ -421,6 +421,163 @@ template <int SW, typename T> __device__ __forceinline__ void seg_argmax2(T p0, 
     wb = b;
 }
 
+// Wave-wide (64-lane) max of a non-negative-or-sentinel T and min of an int: every lane ends with
+// the result (DPP row steps, then the two permlane swaps).
+template <typename T> __device__ __forceinline__ T wave_max64(T m) {
+    using BT = Bits<T>;
+    auto dpp_max = [&](auto ctrl) {
+        constexpr int C = decltype(ctrl)::value;
+        unsigned u[BT::W];
+        BT::split(m, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) u[i] = dpp_u32<C>(u[i]);
+        m = fmax(m, BT::join(u));
+    };
+    auto swap_max = [&](auto which) {
+        unsigned u[BT::W], r0[BT::W], r1[BT::W];
+        BT::split(m, u);
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) {
+            const auto r = decltype(which)::value == 16 ? __builtin_amdgcn_permlane16_swap(u[i], u[i], false, false)
+                                                         : __builtin_amdgcn_permlane32_swap(u[i], u[i], false, false);
+            r0[i] = r[0];
+            r1[i] = r[1];
+        }
+        m = fmax(m, fmax(BT::join(r0), BT::join(r1)));
+    };
+    dpp_max(std::integral_constant<int, 0xB1>{});
+    dpp_max(std::integral_constant<int, 0x4E>{});
+    dpp_max(std::integral_constant<int, 0x141>{});
+    dpp_max(std::integral_constant<int, 0x140>{});
+    swap_max(std::integral_constant<int, 16>{});
+    swap_max(std::integral_constant<int, 32>{});
+    return m;
+}
+__device__ __forceinline__ int wave_min64(int b) {
+    auto dpp_min = [&](auto ctrl) { b = min(b, (int)dpp_u32<decltype(ctrl)::value>((unsigned)b)); };
+    auto swap_min = [&](auto which) {
+        const auto r = decltype(which)::value == 16 ? __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false)
+                                                     : __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+        b = min(b, min((int)r[0], (int)r[1]));
+    };
+    dpp_min(std::integral_constant<int, 0xB1>{});
+    dpp_min(std::integral_constant<int, 0x4E>{});
+    dpp_min(std::integral_constant<int, 0x141>{});
+    dpp_min(std::integral_constant<int, 0x140>{});
+    swap_min(std::integral_constant<int, 16>{});
+    swap_min(std::integral_constant<int, 32>{});
+    return b;
+}
+
+// Top-k of one window by ONE wave over the band staged at xb[j] = X[kmin + j], j < span (lane l
+// holds j = l + 64 i, i < NB), in the reference's order (power desc, bin asc).  Per round: one
+// wave-wide max of the lanes' best powers, then the winning lane from the ballot of lanes holding
+// that max (scalar find-first, no second reduction chain); only a tie between lanes (equal powers)
+// takes the min-over-bins reduction.  Lane r keeps round r's winner; lanes < k write the records
+// at the end (one contiguous 4k-element row).
+template <int NB, typename T>
+__device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span, int k, int lane, T *rec, bool active) {
+    // the lane's NB candidates sorted once (power desc, bin asc): its best is always p[0] and
+    // retiring it is a shift, not a rescan
+    T p[NB];
+    int jj[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int j = lane + 64 * i;
+        T v = T(-1);
+        if (j < span) {
+            const cpx<T> x = xb[j];
+            v = x.re * x.re + x.im * x.im;
+        }
+        p[i] = v;
+        jj[i] = j;
+    }
+    // insertion sort; ascending j within the lane, so strict '>' keeps the lower bin first on ties
+#pragma unroll
+    for (int i = 1; i < NB; ++i) {
+#pragma unroll
+        for (int q = i; q > 0; --q) {
+            const bool sw = p[q] > p[q - 1];
+            const T hi = sw ? p[q] : p[q - 1], lo = sw ? p[q - 1] : p[q];
+            const int jh = sw ? jj[q] : jj[q - 1], jl = sw ? jj[q - 1] : jj[q];
+            p[q - 1] = hi;
+            p[q] = lo;
+            jj[q - 1] = jh;
+            jj[q] = jl;
+        }
+    }
+    T my_p = T(-1);
+    int my_j = -1;
+    const int kk = k < 64 ? k : 64;
+    using BT = Bits<T>;
+    for (int r = 0; r < kk; ++r) {
+        const T bp = p[0];
+        if (__ballot(bp >= T(0)) == 0) break;  // nothing left in range (uniform)
+        // the high word of a non-negative IEEE value orders like the value: max over it (integer DPP
+        // steps), and usually one lane holds that word -> the winner without a second chain
+        unsigned u[BT::W];
+        BT::split(bp, u);
+        const unsigned hi = bp >= T(0) ? u[BT::W - 1] : 0u;
+        unsigned mh = hi;
+        mh = max(mh, dpp_u32<0xB1>(mh));
+        mh = max(mh, dpp_u32<0x4E>(mh));
+        mh = max(mh, dpp_u32<0x141>(mh));
+        mh = max(mh, dpp_u32<0x140>(mh));
+        {
+            const auto r16 = __builtin_amdgcn_permlane16_swap(mh, mh, false, false);
+            mh = max(mh, max((unsigned)r16[0], (unsigned)r16[1]));
+            const auto r32 = __builtin_amdgcn_permlane32_swap(mh, mh, false, false);
+            mh = max(mh, max((unsigned)r32[0], (unsigned)r32[1]));
+        }
+        unsigned long long hold = __ballot(bp >= T(0) && hi == mh);
+        int lw;
+        if (__popcll(hold) == 1) {
+            lw = __ffsll((long long)hold) - 1;
+        } else {  // several lanes share the high word: exact max, then the lowest bin
+            const T m = wave_max64(bp >= T(0) && hi == mh ? bp : T(-1));
+            hold = __ballot(bp == m && bp >= T(0));
+            if (__popcll(hold) == 1) {
+                lw = __ffsll((long long)hold) - 1;
+            } else {
+                const int jm = wave_min64(bp == m ? jj[0] : 0x7fffffff);
+                lw = __builtin_amdgcn_readfirstlane(jm) & 63;
+            }
+        }
+        lw = __builtin_amdgcn_readfirstlane(lw);
+        const int jw = __builtin_amdgcn_readlane(jj[0], lw);
+        unsigned mu[BT::W];
+#pragma unroll
+        for (int i = 0; i < BT::W; ++i) mu[i] = (unsigned)__builtin_amdgcn_readlane((int)u[i], lw);
+        if (lane == r) {
+            my_p = BT::join(mu);
+            my_j = jw;
+        }
+        if (lane == lw) {  // retire the winner: shift the lane's sorted candidates
+#pragma unroll
+            for (int i = 0; i + 1 < NB; ++i) {
+                p[i] = p[i + 1];
+                jj[i] = jj[i + 1];
+            }
+            p[NB - 1] = T(-1);
+        }
+    }
+    if (active && lane < k) {
+        T *o = rec + 4 * lane;
+        if (my_j >= 0) {
+            const cpx<T> x = xb[my_j];
+            o[0] = T(kmin + my_j);
+            o[1] = my_p;
+            o[2] = x.re;
+            o[3] = x.im;
+        } else {  // empty slot
+            o[0] = T(-1);
+            o[1] = T(-1);
+            o[2] = T(0);
+            o[3] = T(0);
+        }
+    }
+}
+
 // k rounds of the top-k scan for one lane holding NB bins kmin + t + TPW i (i < NB).  Round r's
 // winner (power desc, bin asc) goes to on_win(r, wp, wb, own); the owner retires its bin.
 template <int NB, int SW, int TPW, typename T, typename XF, typename WF>
@@ -894,10 +1051,14 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             } else if constexpr (OUT == kOutPower) {
                 prow[ka] = kS2 * (xa.re * xa.re + xa.im * xa.im);
                 prow[kb] = kS2 * (xb.re * xb.re + xb.im * xb.im);
-            } else if constexpr (OUT == kOutTopK || kPhase) {  // stage X for the scan (AoS slot)
+            } else if constexpr (OUT == kOutTopK) {  // stage the scan band X[kmin..kmax] only
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
-                xrow[kPhase ? pad16(ka) : ka] = {kS1 * xa.re, kS1 * xa.im};
-                xrow[kPhase ? pad16(kb) : kb] = {kS1 * xb.re, kS1 * xb.im};
+                if ((unsigned)(ka - a.kmin) <= (unsigned)(a.kmax - a.kmin)) xrow[ka - a.kmin] = {kS1 * xa.re, kS1 * xa.im};
+                if ((unsigned)(kb - a.kmin) <= (unsigned)(a.kmax - a.kmin)) xrow[kb - a.kmin] = {kS1 * xb.re, kS1 * xb.im};
+            } else if constexpr (kPhase) {  // stage X for the phase / scan (AoS slot)
+                cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
+                xrow[pad16(ka)] = {kS1 * xa.re, kS1 * xa.im};
+                xrow[pad16(kb)] = {kS1 * xb.re, kS1 * xb.im};
             } else if (active) {  // packed: (Re, Im) of one bin is already one 16-B (8-B) store
                 v2 oa, ob;
                 oa.x = kS1 * xa.re;
@@ -955,10 +1116,28 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             constexpr int SW = TPW < 64 ? TPW : 64;
             constexpr int kNone = 0x7fffffff;
             constexpr int RW = OUT == kOutTopKPhase ? 6 : 4;  // record width
-            auto xi = [](int k) { return kPhase ? pad16(k) : k; };
+            const int kmin0 = a.kmin;
+            auto xi = [&](int k) { return kPhase ? pad16(k) : k - kmin0; };  // kOutTopK stages the band only
             __syncthreads();  // X row complete
             const int span = a.kmax - a.kmin + 1;
             T *recw = a.out + w * (int64_t)(RW * a.topk);
+            if constexpr (OUT == kOutTopK && TPW >= 64) {
+                // one wave scans the window's whole band (<= 512 bins, 8 per lane): no cross-wave merge.
+                // The split-exchange instantiation carries only this path (the host sends wider bands to
+                // the AoS one), which keeps it within the 168 VGPRs of 3 waves per SIMD.
+                if ((VAR & kVarSplitLds) || span <= 64 * 8) {
+                    if (t < 64) {
+                        const cpx<T> *xb = xrow;
+                        const int nb = (span + 63) / 64;
+                        if (nb <= 1) topk_wave64<1, T>(xb, a.kmin, span, a.topk, t, recw, active);
+                        else if (nb <= 2) topk_wave64<2, T>(xb, a.kmin, span, a.topk, t, recw, active);
+                        else if (nb <= 4) topk_wave64<4, T>(xb, a.kmin, span, a.topk, t, recw, active);
+                        else topk_wave64<8, T>(xb, a.kmin, span, a.topk, t, recw, active);
+                    }
+                    continue;  // next group (its first exchange barrier orders this scan's LDS reads)
+                }
+            }
+            if constexpr (!(OUT == kOutTopK && TPW >= 64 && (VAR & kVarSplitLds))) {
             auto write_x = [&](T *rec, int b, T pw_) {
                 const cpx<T> x = xrow[xi(b)];
                 rec[0] = T(b);
@@ -1065,6 +1244,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 else if (need <= 8 * TPW) add_phase(std::integral_constant<int, 8>{});
                 else add_phase(std::integral_constant<int, 16>{});
             }
+            }  // !(split one-wave top-k)
         }
         if constexpr (OUT == kOutPower && !kDirect) {
             // write the row back with contiguous 16-B stores (1 KiB per wave instruction)

@@ -82,10 +82,22 @@ template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var
     // N > 4096 runs one 256/512-thread workgroup per window, where the split exchange cannot
     // raise occupancy (LDS and VGPRs allow 2 waves/SIMD either way)
     // (the phase outputs keep the round-1 starting point: their register budget is the tightest)
+    // (the top-k scan stages only its band, which fits the split slot when it spans at most about half
+    // of the bins: dispatch_win falls back to the AoS slot for wider bands)
+    // (top-k: the split exchange where one wave scans the band, N = 2048 / 4096 without detrend;
+    // elsewhere its scan paths spill at 168 VGPRs)
+    if constexpr (OUT == kOutTopK)
+        return (DETREND == kDetrendNone && (LOG2N == 11 || LOG2N == 12)) ? kDefaultVar : kCommonVar;
     return (OUT == kOutPhase || OUT == kOutTopKPhase) ? (kVarNoPrefetch | kVarNtStore)
            : (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
                ? kCommonVar
                : kDefaultVar;
+}
+// Can the split-exchange top-k instantiation take a band of `span` bins?  Its one-wave scan holds
+// at most 8 bins per lane, and the band is staged in the window's split slot (SLOT elements of T).
+template <typename T, int LOG2N, int VAR> constexpr bool band_fits(int span) {
+    return !(VAR & kVarSplitLds) ||
+           (span <= 64 * 8 && (int64_t)span * (int64_t)sizeof(cpx<T>) <= (int64_t)Geo<LOG2N>::SLOT * (int64_t)sizeof(T));
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
@@ -103,6 +115,16 @@ hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
 template <typename T, int LOG2N, int DETREND, int OUT>
 hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
     double a0, a1, a2;
+    if constexpr (OUT == kOutTopK && (default_var<T, LOG2N, DETREND, OUT>() & kVarSplitLds) != 0) {
+        if (!band_fits<T, LOG2N, default_var<T, LOG2N, DETREND, OUT>()>(L.kmax - L.kmin + 1)) {
+            switch (window_class(L.window, &a0, &a1, &a2)) {
+            case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos, kCommonVar>(L, s);
+            case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2, kCommonVar>(L, s);
+            case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett, kCommonVar>(L, s);
+            default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone, kCommonVar>(L, s);
+            }
+        }
+    }
     switch (window_class(L.window, &a0, &a1, &a2)) {
     case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos>(L, s);
     case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2>(L, s);

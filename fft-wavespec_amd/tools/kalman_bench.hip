@@ -31,12 +31,19 @@ using namespace wsp;
 
 static const double kDefaults[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
 
-// launch one variant: WAVES = 4 adds the one-workgroup-per-CU LDS reservation
-template <typename T, int J, int FL, bool TWO, int WAVES, bool PK = false>
+static unsigned *g_fallbacks = nullptr;  // waves that re-ran their second segments (SEG = 2)
+static double *g_dbg = nullptr;
+static void dump_dbg(const char *name, int64_t W);          // SEG = 2: per window [exact state (14) | warm-up state (14)]
+
+// launch one variant: WAVES = 4 adds the one-workgroup-per-CU LDS reservation (two per CU for SEG = 2)
+template <typename T, int J, int FL, bool TWO, int WAVES, bool PK = false, int SEG = 1, int WU = kcore::kSegWarm>
 void launch(const T *x, T *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
-    const size_t reserve = WAVES == 4 ? 84 * 1024 - 4 * 64 * (J + 1) * sizeof(T) : 0;
-    hipLaunchKernelGGL((kcore::kalman_detrend_kernel<T, T, J, 64, J, FL, TWO, WAVES, PK>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)),
-                       dim3(64 * WAVES), reserve, s, x, d, hop, W, n, kp);
+    constexpr int WPW = SEG == 2 ? 32 : 64;
+    const size_t stat = 4 * 64 * (J + 1) * sizeof(T);
+    const size_t reserve = WAVES == 4 ? (SEG == 2 ? 78 : 84) * 1024 - stat : 0;
+    hipLaunchKernelGGL((kcore::kalman_detrend_kernel<T, T, J, WPW, J, FL, TWO, WAVES, PK, SEG, WU>),
+                       dim3((W + WPW * WAVES - 1) / (WPW * WAVES)), dim3(64 * WAVES), reserve, s, x, d, hop, W, n, kp,
+                       g_fallbacks, g_dbg);
 }
 
 __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n) {
@@ -44,7 +51,7 @@ __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ i
         out[j] = in[j];
 }
 
-template <int FL, bool TWO, int WAVES, bool PK = false>
+template <int FL, bool TWO, int WAVES, bool PK = false, int SEG = 1, int WU = kcore::kSegWarm>
 void time_variant(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n,
                   int reps, hipStream_t s) {
     kcore::KP kp;
@@ -53,9 +60,9 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventCreate(&c));
-    launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
+    launch<float, 32, FL, TWO, WAVES, PK, SEG, WU>(x, d, n, W, n, kp, s);
     CK(hipEventRecord(a, s));
-    for (int r = 0; r < reps; ++r) launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
+    for (int r = 0; r < reps; ++r) launch<float, 32, FL, TWO, WAVES, PK, SEG, WU>(x, d, n, W, n, kp, s);
     CK(hipEventRecord(b, s));
     CK(hipEventSynchronize(b));
     float back, alt = 0;
@@ -63,7 +70,7 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     for (int r = 0; r < reps; ++r) {
         hipLaunchKernelGGL(stream_copy, dim3(8192), dim3(256), 0, s, ci, co, cn);
         CK(hipEventRecord(a, s));
-        launch<float, 32, FL, TWO, WAVES, PK>(x, d, n, W, n, kp, s);
+        launch<float, 32, FL, TWO, WAVES, PK, SEG, WU>(x, d, n, W, n, kp, s);
         CK(hipEventRecord(c, s));
         CK(hipEventSynchronize(c));
         float t;
@@ -104,6 +111,21 @@ int time_main(int reps) {
         time_variant<3, true, 4>("4-wave WG + 1 WG/CU, static, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<kcore::kKfRuntime, true, 4>("4-wave WG + 1 WG/CU, runtime, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<3, true, 4, true>("4-wave WG + 1 WG/CU, static, packed update", x, d, ci, co, cn, W, n, reps, s);
+        auto seg = [&](auto wu) {
+            constexpr int WU = decltype(wu)::value;
+            CK(hipMemset(g_fallbacks, 0, 4));
+            char nm[96];
+            snprintf(nm, sizeof nm, "2 segments WU=%d, 4-wave WG + 2 WG/CU", WU);
+            time_variant<3, true, 4, true, 2, WU>(nm, x, d, ci, co, cn, W, n, reps, s);
+            unsigned fb = 0;
+            CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+            printf("    fallbacks: %u waves of %lld over %d launches\n", fb, (long long)(W / 32), 1 + 2 * reps);
+            dump_dbg(nm, W);
+        };
+        seg(std::integral_constant<int, 256>{});
+        seg(std::integral_constant<int, 512>{});
+        seg(std::integral_constant<int, 768>{});
+        seg(std::integral_constant<int, 1024>{});
     }
     return 0;
 }
@@ -155,13 +177,13 @@ static void host_kalman(const double *x, int n, const double *kp, double *d) {
     }
 }
 
-template <int FL, bool TWO, int WAVES>
+template <int FL, bool TWO, int WAVES, int SEG = 1>
 void check_one(const char *name, const double *dx, double *dd, const std::vector<double> &ref, int64_t W, int64_t hop, int n,
                const double *kpa) {
     kcore::KP kp;
     memcpy(&kp, kpa, sizeof(kp));
     CK(hipMemset(dd, 0xff, (W + 300) * n * 8));  // NaN canary past the batch end as well
-    launch<double, 16, FL, TWO, WAVES>(dx, dd, hop, W, n, kp, 0);
+    launch<double, 16, FL, TWO, WAVES, false, SEG>(dx, dd, hop, W, n, kp, 0);
     CK(hipDeviceSynchronize());
     std::vector<double> h((W + 300) * n);
     CK(hipMemcpy(h.data(), dd, h.size() * 8, hipMemcpyDeviceToHost));
@@ -178,7 +200,7 @@ void check_one(const char *name, const double *dx, double *dd, const std::vector
 }
 
 // fp32 filter (and the packed update) against the same host restatement: relative to the residual scale
-template <bool PK>
+template <bool PK, int SEG = 1>
 void check_f32(const char *name, const std::vector<double> &x, const std::vector<double> &ref, int64_t W, int64_t hop, int n) {
     kcore::KP kp;
     memcpy(&kp, kDefaults, sizeof(kp));
@@ -187,7 +209,7 @@ void check_f32(const char *name, const std::vector<double> &x, const std::vector
     CK(hipMalloc(&dx, xf.size() * 4));
     CK(hipMalloc(&dd, W * n * 4));
     CK(hipMemcpy(dx, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
-    launch<float, 32, 3, true, 4, PK>(dx, dd, hop, W, n, kp, 0);
+    launch<float, 32, 3, true, 4, PK, SEG>(dx, dd, hop, W, n, kp, 0);
     CK(hipDeviceSynchronize());
     std::vector<float> h(W * n);
     CK(hipMemcpy(h.data(), dd, W * n * 4, hipMemcpyDeviceToHost));
@@ -201,9 +223,32 @@ void check_f32(const char *name, const std::vector<double> &x, const std::vector
     CK(hipFree(dd));
 }
 
-int check_main() {
+// per state component: max |exact - warm| and max |exact| over the windows of the last SEG = 2 launch
+static void dump_dbg(const char *name, int64_t W) {
+    std::vector<double> h(W * 28);
+    CK(hipMemcpy(h.data(), g_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    static const char *nm[14] = {"pos", "vel", "acc", "jerk", "p00", "p01", "p02", "p03", "p11", "p12", "p13", "p22", "p23", "p33"};
+    int64_t same = 0;
+    for (int64_t w = 0; w < W; ++w) {
+        bool eq = true;
+        for (int k = 0; k < 14; ++k) eq = eq && h[w * 28 + k] == h[w * 28 + 14 + k];
+        same += eq;
+    }
+    printf("    %s: %lld of %lld windows bit-identical after the warm-up\n", name, (long long)same, (long long)W);
+    printf("    %s state |exact - warm| / |exact|:", name);
+    for (int k = 0; k < 14; ++k) {
+        double md = 0, mv = 0;
+        for (int64_t w = 0; w < W; ++w) {
+            md = fmax(md, fabs(h[w * 28 + k] - h[w * 28 + 14 + k]));
+            mv = fmax(mv, fabs(h[w * 28 + k]));
+        }
+        printf(" %s %.2e/%.2e", nm[k], md, mv);
+    }
+    printf("\n");
+}
+
+int check_main(int n) {
     const int64_t W = 100, hop = 37;
-    const int n = 256;
     const int64_t len = (W - 1) * hop + n;
     std::vector<double> x(len);
     double v = 1.1;
@@ -221,6 +266,14 @@ int check_main() {
     check_one<kcore::kKfRuntime, true, 1>("1-wave runtime two-stage", dx, dd, ref, W, hop, n, kDefaults);
     check_one<3, true, 1>("1-wave static two-stage", dx, dd, ref, W, hop, n, kDefaults);
     check_one<3, true, 4>("4-wave static two-stage", dx, dd, ref, W, hop, n, kDefaults);
+    if (n >= 1024) {
+        CK(hipMemset(g_fallbacks, 0, 4));
+        check_one<3, true, 4, 2>("2 segments static two-stage", dx, dd, ref, W, hop, n, kDefaults);
+        unsigned fb = 0;
+        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+        printf("    2-segment fallbacks (f64): %u of %lld waves\n", fb, (long long)((W + 31) / 32));
+        dump_dbg("f64", W);
+    }
     double ema[16];
     memcpy(ema, kDefaults, sizeof(ema));
     ema[15] = 12.0;
@@ -231,11 +284,22 @@ int check_main() {
     for (int64_t w = 0; w < W; ++w) host_kalman(&xr[w * hop], n, kDefaults, &ref[w * n]);
     check_f32<false>("f32 4-wave static two-stage", xr, ref, W, hop, n);
     check_f32<true>("f32 4-wave static packed update", xr, ref, W, hop, n);
+    if (n >= 1024) {
+        CK(hipMemset(g_fallbacks, 0, 4));
+        check_f32<true, 2>("f32 2 segments packed update", xr, ref, W, hop, n);
+        unsigned fb = 0;
+        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+        printf("    2-segment fallbacks (f32): %u of %lld waves\n", fb, (long long)((W + 31) / 32));
+        dump_dbg("f32", W);
+    }
     return 0;
 }
 
 int main(int argc, char **argv) {
     const std::string mode = argc > 1 ? argv[1] : "time";
-    if (mode == "check") return check_main();
+    CK(hipMalloc(&g_fallbacks, 4));
+    CK(hipMemset(g_fallbacks, 0, 4));
+    CK(hipMalloc(&g_dbg, 65536 * 28 * 8));
+    if (mode == "check") return check_main(argc > 2 ? atoi(argv[2]) : 256);
     return time_main(argc > 2 ? atoi(argv[2]) : 10);
 }

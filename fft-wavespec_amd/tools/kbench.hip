@@ -154,8 +154,16 @@ int out_main(int reps) {
         L.kmax = 227;
         const float ph = time_out<kOutPhase, AOS>(L, s, reps);
         const float tp = time_out<kOutTopKPhase, AOS>(L, s, reps);
+        // library defaults: power and top-k (band-staged, one-wave scan) on the split exchange
+        const float pd = time_out<kOutPower, kDefaultVar>(L, s, reps);
+        const float td = time_out<kOutTopK, kDefaultVar>(L, s, reps);
+        L.topk = 0;
+        const float td0 = time_out<kOutTopK, kDefaultVar>(L, s, reps);
+        L.topk = 8;
+        const float tc = time_out<kOutTopK, kCommonVar>(L, s, reps);
         printf("round %d  power-aos %.1f  power-split %.1f  packed %.1f | topk k=0 %.1f  k=1 %.1f  k=8 %.1f  "
-               "k=8/2 bins %.1f | phase %.1f  topk-phase %.1f us\n", round, pa, ps, pk, t0, t1, t8, t8n, ph, tp);
+               "k=8/2 bins %.1f | phase %.1f  topk-phase %.1f us | library: power %.1f  topk k=8 %.1f (k=0 %.1f, "
+               "AoS slot %.1f)\n", round, pa, ps, pk, t0, t1, t8, t8n, ph, tp, pd, td, td0, tc);
         fflush(stdout);
     }
     return 0;

@@ -158,11 +158,107 @@ def batch_topk_phase(series, n, hop, detrend="none", window="hann", trend_period
 
 
 # ---------------------------------------------------------------- numpy cross-check
-def numpy_spectrum(x, detrend="none", window="hann", trend_period=0) -> np.ndarray:
+def numpy_kalman_trend(X, params=None) -> np.ndarray:
+    """Second, independent transliteration of ResetKalmanState / StepKalman4D
+    (L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:2015-2029 / :2031-2125), vectorised over windows:
+    X is (W, n) or (n,); every window is reset with its first sample and stepped over all of its
+    samples (the per-window discipline of wavespec_oracle.c ora_kalman_trend).  Expression order
+    follows the MQL5 source statement by statement, including the full 16-entry covariance and
+    the P11 prediction of :2052; shares no code with the C oracle."""
+    kp = KALMAN_DEFAULTS if params is None else list(params)
+    (follow, q_pos, q_vel, q_acc, q_jerk, adapt_gain, meas_noise, var_pos, var_vel, var_acc, var_jerk, init_vel,
+     init_acc, init_jerk, clip_std, ema_period) = [float(v) for v in kp]
+    X = np.asarray(X, dtype=np.float64)
+    one = X.ndim == 1
+    X = np.atleast_2d(X)
+    W, n = X.shape
+    # ResetKalmanState(first_meas) :2015-2029
+    pos, vel = X[:, 0].copy(), np.full(W, init_vel)
+    acc, jerk = np.full(W, init_acc), np.full(W, init_jerk)
+    P = np.zeros((W, 4, 4))
+    P[:, 0, 0], P[:, 1, 1] = max(1e-9, var_pos), max(1e-9, var_vel)
+    P[:, 2, 2], P[:, 3, 3] = max(1e-9, var_acc), max(1e-9, var_jerk)
+    ema_ready, ema_prev = False, np.zeros(W)
+    q_scale = max(0.05, follow)
+    Qp, Qv = max(1e-9, q_pos * q_scale), max(1e-9, q_vel * q_scale)
+    Qa, Qj = max(1e-9, q_acc * q_scale), max(1e-9, q_jerk * q_scale)
+    R = max(1e-9, meas_noise)
+    trend = np.empty((W, n))
+    g = lambda i, j: P[:, i, j]  # noqa: E731
+    for t in range(n):
+        z = X[:, t]
+        x0p = pos + vel + 0.5 * acc + (1.0 / 6.0) * jerk
+        x1p = vel + acc + 0.5 * jerk
+        x2p = acc + jerk
+        x3p = jerk
+        P00p = (g(0, 0) + g(0, 1) + 0.5 * g(0, 2) + (1.0 / 6.0) * g(0, 3)
+                + g(1, 0) + g(1, 1) + 0.5 * g(1, 2) + (1.0 / 6.0) * g(1, 3)
+                + 0.5 * g(2, 0) + 0.5 * g(2, 1) + 0.25 * g(2, 2) + (1.0 / 12.0) * g(2, 3)
+                + (1.0 / 6.0) * g(3, 0) + (1.0 / 6.0) * g(3, 1) + (1.0 / 12.0) * g(3, 2) + (1.0 / 36.0) * g(3, 3)
+                + Qp)
+        P01p = (g(0, 1) + g(0, 2) + 0.5 * g(0, 3) + g(1, 1) + g(1, 2) + 0.5 * g(1, 3) + 0.5 * g(2, 1) + 0.5 * g(2, 2)
+                + 0.25 * g(2, 3) + (1.0 / 6.0) * g(3, 1) + (1.0 / 6.0) * g(3, 2) + (1.0 / 12.0) * g(3, 3))
+        P02p = (g(0, 2) + g(0, 3) + g(1, 2) + g(1, 3) + 0.5 * g(2, 2) + 0.5 * g(2, 3) + (1.0 / 6.0) * g(3, 2)
+                + (1.0 / 6.0) * g(3, 3))
+        P03p = g(0, 3) + g(1, 3) + 0.5 * g(2, 3) + (1.0 / 6.0) * g(3, 3)
+        P11p = (g(1, 1) + 2.0 * g(1, 2) + g(1, 3) + g(2, 1) + 2.0 * g(2, 2) + g(2, 3) + 0.5 * g(3, 1) + 0.5 * g(3, 2)
+                + 0.25 * g(3, 3) + Qv)
+        P12p = g(1, 2) + g(1, 3) + g(2, 2) + g(2, 3) + 0.5 * g(3, 2) + 0.5 * g(3, 3)
+        P13p = g(1, 3) + g(2, 3) + 0.5 * g(3, 3)
+        P22p = g(2, 2) + 2.0 * g(2, 3) + g(3, 3) + Qa
+        P23p = g(2, 3) + g(3, 3)
+        P33p = g(3, 3) + Qj
+        P10p, P20p, P30p, P21p, P31p, P32p = P01p, P02p, P03p, P12p, P13p, P23p
+        y = z - x0p
+        S = P00p + R
+        if adapt_gain > 0.0:
+            sigma = np.sqrt(S)
+            k = np.minimum(5.0, np.abs(y) / sigma) * adapt_gain
+            boost = 1.0 + k
+            P00p = P00p + (boost - 1.0) * Qp
+            P11p = P11p + (boost - 1.0) * Qv
+            P22p = P22p + (boost - 1.0) * Qa
+            P33p = P33p + (boost - 1.0) * Qj
+            S = P00p + R
+        if clip_std > 0.0:
+            lim = clip_std * np.sqrt(S)
+            y = np.where(y > lim, lim, y)
+            y = np.where(y < -lim, -lim, y)
+        K0, K1, K2, K3 = P00p / S, P10p / S, P20p / S, P30p / S
+        pos = x0p + K0 * y
+        vel = x1p + K1 * y
+        acc = x2p + K2 * y
+        jerk = x3p + K3 * y
+        rows = ((P00p, P01p, P02p, P03p), (P10p, P11p, P12p, P13p), (P20p, P21p, P22p, P23p),
+                (P30p, P31p, P32p, P33p))
+        Kv = (K0, K1, K2, K3)
+        Pn = np.empty_like(P)
+        for j in range(4):
+            Pn[:, 0, j] = (1.0 - K0) * rows[0][j]
+        for i in range(1, 4):
+            for j in range(4):
+                Pn[:, i, j] = rows[i][j] - Kv[i] * rows[0][j]
+        for i in range(4):
+            Pn[:, i, i] = np.maximum(1e-12, Pn[:, i, i])
+        P = Pn
+        out = pos
+        if ema_period > 0.0:  # :2117-2123
+            alpha = 2.0 / (ema_period + 1.0)
+            if not ema_ready:
+                ema_prev, ema_ready = out.copy(), True
+            ema_prev = alpha * out + (1.0 - alpha) * ema_prev
+            out = ema_prev
+        trend[:, t] = out
+    return trend[0] if one else trend
+
+
+def numpy_spectrum(x, detrend="none", window="hann", trend_period=0, kalman=None) -> np.ndarray:
     """Independent numpy restatement (no shared code with the C oracle)."""
     x = np.asarray(x, dtype=np.float64)
     n = x.size
-    if detrend == "mean":
+    if detrend == "kalman":
+        d = x - numpy_kalman_trend(x, kalman)
+    elif detrend == "mean":
         d = x - x.mean()
     elif detrend == "iir" and trend_period > 0:
         om = 2 * np.pi / trend_period
