@@ -47,12 +47,13 @@ def main():
                                       kalman=oracle.KALMAN_DEFAULTS)
         packed = oracle.batch_spectrum(s, c["n"], c["hop"], c["detrend"], c["window"], c["trend_period"],
                                        kalman=oracle.KALMAN_DEFAULTS, output="packed")
-        if c["detrend"] != "kalman":
-            nwin = power.shape[0]
-            ref = np.stack([oracle.numpy_spectrum(s[w * c["hop"]: w * c["hop"] + c["n"]], c["detrend"], c["window"],
-                                                  c["trend_period"]) for w in range(nwin)])
-            err = oracle.rel_err(power, ref)
-            assert err < 1e-10, (name, err)  # the parity bar; observed <= 3e-12
+        # independent numpy restatement (Kalman: oracle.numpy_kalman_trend, a second transliteration of
+        # StepKalman4D) for every case
+        nwin = power.shape[0]
+        ref = np.stack([oracle.numpy_spectrum(s[w * c["hop"]: w * c["hop"] + c["n"]], c["detrend"], c["window"],
+                                              c["trend_period"], kalman=oracle.KALMAN_DEFAULTS) for w in range(nwin)])
+        err = oracle.rel_err(power, ref)
+        assert err < 1e-10, (name, err)  # the parity bar; observed <= 3e-12
         np.savez_compressed(OUT / f"{name}.npz", series=s, n=c["n"], hop=c["hop"], detrend=c["detrend"],
                             window=c["window"], trend_period=c["trend_period"],
                             kalman=np.asarray(oracle.KALMAN_DEFAULTS), power=power, packed=packed)

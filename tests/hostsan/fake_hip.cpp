@@ -1,0 +1,248 @@
+// fake_hip.cpp -- TEST DOUBLE of the HIP runtime calls and kernel launches that
+// fft-wavespec_amd/csrc/mtbridge.cpp makes, for sanitizer builds of the host
+// layer on a machine without a GPU ("TSAN on the host harness, ASAN
+// builds").  Never linked into the product: tests/hostsan/Makefile builds
+// mtbridge.cpp + this file into a separate libmtbridge_{tsan,asan}.so.
+//
+// Streams are real asynchronous queues (one worker thread each), so copies,
+// "kernels" and event completions run concurrently with the calling threads,
+// as on the device: the sanitizers see the same cross-thread hand-offs as the
+// real runtime would impose (job copy-out vs completion, session teardown vs
+// calls in flight, plan destroy vs execute).  "Device" memory is host memory.
+// The launch stubs write a deterministic function of each window's own input
+// samples, so a driver can check that every record was routed to the right
+// place: record element k of window w = series[w*hop + k % N] + k.
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+#include "../../fft-wavespec_amd/csrc/wsp_internal.h"
+
+struct ihipStream_t {
+    std::mutex mu;
+    std::condition_variable cv, idle;
+    std::deque<std::function<void()>> q;
+    bool stop = false, busy = false;
+    std::thread worker;
+    ihipStream_t() {
+        worker = std::thread([this] {
+            std::unique_lock<std::mutex> lk(mu);
+            for (;;) {
+                cv.wait(lk, [this] { return stop || !q.empty(); });
+                if (q.empty() && stop) break;
+                auto f = std::move(q.front());
+                q.pop_front();
+                busy = true;
+                lk.unlock();
+                f();
+                lk.lock();
+                busy = false;
+                if (q.empty()) idle.notify_all();
+            }
+        });
+    }
+    void push(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(std::move(f));
+        }
+        cv.notify_one();
+    }
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu);
+        idle.wait(lk, [this] { return q.empty() && !busy; });
+    }
+    ~ihipStream_t() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_one();
+        worker.join();
+    }
+};
+
+struct ihipEvent_t {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t recorded = 0, reached = 0;
+};
+
+namespace {
+std::mutex g_streams_mu;
+std::deque<ihipStream_t *> g_streams;  // live streams, for hipDeviceSynchronize
+thread_local int t_device = 0;
+int n_devices() {
+    const char *e = getenv("WSP_FAKE_DEVICES");
+    return e ? atoi(e) : 1;
+}
+// the null stream: executes synchronously on the caller
+void run_on(hipStream_t s, std::function<void()> f) {
+    if (s) s->push(std::move(f));
+    else f();
+}
+}  // namespace
+
+extern "C" {
+hipError_t hipGetDeviceCount(int *n) {
+    *n = n_devices();
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int d) {
+    if (d < 0 || d >= n_devices()) return hipErrorInvalidDevice;
+    t_device = d;
+    return hipSuccess;
+}
+hipError_t hipMalloc(void **p, size_t n) {
+    *p = aligned_alloc(256, (n + 255) & ~size_t(255));
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFree(void *p) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipHostMalloc(void **p, size_t n, unsigned int) { return hipMalloc(p, n); }
+hipError_t hipHostFree(void *p) { return hipFree(p); }
+hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int) {
+    *d = h;
+    return hipSuccess;
+}
+hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
+    memcpy(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t st) {
+    run_on(st, [=] { memcpy(d, s, n); });
+    return hipSuccess;
+}
+hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int) {
+    *s = new ihipStream_t();
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    g_streams.push_back(*s);
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t s) {
+    if (s) s->drain();
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s) {
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        for (auto it = g_streams.begin(); it != g_streams.end(); ++it)
+            if (*it == s) {
+                g_streams.erase(it);
+                break;
+            }
+    }
+    s->drain();
+    delete s;
+    return hipSuccess;
+}
+hipError_t hipDeviceSynchronize(void) {
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    for (auto *s : g_streams) s->drain();
+    return hipSuccess;
+}
+hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned int) {
+    *e = new ihipEvent_t();
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e) {
+    delete e;
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+    uint64_t gen;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        gen = ++e->recorded;
+    }
+    run_on(s, [e, gen] {
+        {
+            std::lock_guard<std::mutex> lk(e->mu);
+            if (gen > e->reached) e->reached = gen;
+        }
+        e->cv.notify_all();
+    });
+    return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t e) {
+    std::lock_guard<std::mutex> lk(e->mu);
+    return e->reached >= e->recorded ? hipSuccess : hipErrorNotReady;
+}
+hipError_t hipEventSynchronize(hipEvent_t e) {
+    std::unique_lock<std::mutex> lk(e->mu);
+    e->cv.wait(lk, [e] { return e->reached >= e->recorded; });
+    return hipSuccess;
+}
+const char *hipGetErrorString(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "fake hip error"; }
+}  // extern "C"
+
+// ---- kernel launch stubs (wsp_internal.h): record element k of window w = x_w[k % N] + k
+namespace wsp {
+namespace {
+template <typename T> void fill(const void *series, int64_t hop, int n, int64_t nw, int64_t rec, void *out) {
+    const T *x = static_cast<const T *>(series);
+    T *o = static_cast<T *>(out);
+    for (int64_t w = 0; w < nw; ++w)
+        for (int64_t k = 0; k < rec; ++k) o[w * rec + k] = x[w * hop + k % n] + (T)k;
+}
+int64_t record_of(int n, int output, int topk) {
+    switch (output) {
+    case kOutPacked: return n;
+    case kOutTopK: return 4 * topk;
+    case kOutPhase: return 3 * (n / 2);
+    case kOutTopKPhase: return 6 * topk;
+    default: return n / 2;
+    }
+}
+}  // namespace
+
+hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t s) {
+    const SpectrumLaunch c = L;
+    run_on(s, [c] {
+        const int n = 1 << c.log2n;
+        const int64_t rec = record_of(n, c.output, c.topk);
+        if (c.f32) fill<float>(c.series, c.hop, n, c.n_windows, rec, c.out);
+        else fill<double>(c.series, c.hop, n, c.n_windows, rec, c.out);
+    });
+    return hipSuccess;
+}
+hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
+hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
+hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // detrended = the window itself
+    const KalmanLaunch c = L;
+    run_on(s, [c] {
+        const size_t es = c.f32 ? 4 : 8;
+        for (int64_t w = 0; w < c.n_windows; ++w)
+            memcpy(static_cast<char *>(c.detrended) + (size_t)(w * c.n) * es,
+                   static_cast<const char *>(c.series) + (size_t)(w * c.hop) * es, (size_t)c.n * es);
+    });
+    return hipSuccess;
+}
+hipError_t launch_inverse(const InverseLaunch &L, hipStream_t s) {
+    const InverseLaunch c = L;
+    run_on(s, [c] { fill<double>(c.in, int64_t(1) << c.log2n, 1 << c.log2n, c.n_windows, int64_t(1) << c.log2n, c.out); });
+    return hipSuccess;
+}
+hipError_t launch_phase_row(const double *spec, int n_bins, int, double *out, hipStream_t s) {
+    run_on(s, [=] { fill<double>(spec, 0, 2 * n_bins, 1, n_bins, out); });
+    return hipSuccess;
+}
+hipError_t launch_large(const LargeLaunch &L, hipStream_t s) {
+    const LargeLaunch c = L;
+    run_on(s, [c] {
+        const int n = 1 << c.log2n;
+        fill<double>(c.series, c.hop, n, c.n_windows, c.packed ? n : n / 2, c.out);
+    });
+    return hipSuccess;
+}
+int64_t large_chunk(int, bool) { return 64; }
+}  // namespace wsp

@@ -1,0 +1,196 @@
+// stress.cpp -- concurrency driver of the C ABI for the sanitizer builds
+// (tests/hostsan/Makefile: mtbridge.cpp + the fake_hip.cpp test double, built
+// with -fsanitize=thread or -fsanitize=address,undefined).  It dlopen()s the
+// library like the MT5 terminal (Include/imports.mqh:4) and replays, from many
+// threads at once, the call sequences the reference makes:
+//   * 28 charts (WaveCyclesBatchFetcher.mq5:104-133 / 1.1.0:722-757, 706-716):
+//     gpu_init, submit + poll + free batch jobs, per-bar gpu_fft_real_forward,
+//     then gpu_shutdown -- half of them early, while the others keep working;
+//   * a poller racing gpu_free_job on the same job;
+//   * device plans executed while another thread re-targets (set_topk) and
+//     destroys them;
+//   * gpu_init on another device while the session is open (must be refused).
+// Every record is checked against the fake kernels' formula
+// (record element k of window w = x[w*hop + k % N] + k).  Exit 0 = all good.
+#include <dlfcn.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/mtbridge.h"
+
+namespace {
+struct Api {
+    decltype(&gpu_init) init;
+    decltype(&gpu_shutdown) shutdown;
+    decltype(&gpu_fft_real_forward) fft;
+    decltype(&gpu_submit_spectrum_batch) submit;
+    decltype(&gpu_try_get_spectrum_batch) try_get;
+    decltype(&gpu_free_job) free_job;
+    decltype(&gpu_spectrum_batch) batch;
+    decltype(&wsp_plan_create) plan_create;
+    decltype(&wsp_plan_execute) plan_execute;
+    decltype(&wsp_plan_set_topk) plan_set_topk;
+    decltype(&wsp_plan_destroy) plan_destroy;
+} A;
+std::atomic<int> g_fail{0};
+
+#define CHECK(c, ...)                              \
+    do {                                           \
+        if (!(c)) {                                \
+            fprintf(stderr, "FAIL %s:%d ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);          \
+            fprintf(stderr, "\n");                 \
+            g_fail++;                              \
+        }                                          \
+    } while (0)
+
+template <typename F> void sym(void *h, F &f, const char *n) {
+    f = reinterpret_cast<F>(dlsym(h, n));
+    if (!f) {
+        fprintf(stderr, "missing %s\n", n);
+        exit(3);
+    }
+}
+
+std::vector<double> series_of(int sym, int len) {
+    std::vector<double> s(len);
+    for (int i = 0; i < len; ++i) s[i] = 1.0 + 0.001 * sym + 1e-6 * (double)((i * 7919) % 1000);
+    return s;
+}
+
+bool check_records(const std::vector<double> &s, const double *out, int n, int hop, int nrec, int rec) {
+    for (int w = 0; w < nrec; ++w)
+        for (int k = 0; k < rec; ++k)
+            if (out[(size_t)w * rec + k] != s[(size_t)w * hop + k % n] + (double)k) return false;
+    return true;
+}
+
+// one chart: EnsureGpu, batch jobs + live per-bar calls, OnDeinit
+void chart(int sym, bool early, std::atomic<int> &early_done, int rounds) {
+    CHECK(A.init(0, 16) == MTB_OK, "init sym %d", sym);
+    const int n = 64 << (sym % 4), hop = 1 + sym % 3, len = 40 * hop + n;
+    const std::vector<double> s = series_of(sym, len);
+    const int nwin = 1 + (len - n) / hop, rec = n / 2;
+    std::vector<double> out((size_t)nwin * rec);
+    for (int r = 0; r < rounds; ++r) {
+        if (early && r == rounds / 2) {
+            A.shutdown();  // this chart closes mid-way; the others must keep their session
+            early_done++;
+            return;
+        }
+        int64_t jid = 0;
+        CHECK(A.submit(s.data(), len, n, hop, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, &jid) == MTB_OK &&
+                  jid > 0, "submit sym %d round %d", sym, r);
+        int ready = 0, got = 0, st = MTB_NOT_READY;
+        for (int p = 0; p < 100000 && !ready; ++p) {
+            st = A.try_get(jid, out.data(), (int)out.size(), &got, &ready);
+            if (!ready) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        CHECK(st == MTB_OK && ready == 1 && got == nwin, "poll sym %d st %d ready %d got %d", sym, st, ready, got);
+        CHECK(check_records(s, out.data(), n, hop, nwin, rec), "records sym %d round %d", sym, r);
+        CHECK(A.free_job(jid) == MTB_OK, "free sym %d", sym);
+        std::vector<double> win(s.begin(), s.begin() + n), packed(n);  // per-bar live call (1.1.0:1249)
+        CHECK(A.fft(win.data(), n, packed.data()) == MTB_OK, "live sym %d", sym);
+        CHECK(check_records(win, packed.data(), n, n, 1, n), "live records sym %d", sym);
+    }
+    A.shutdown();
+}
+
+void free_race() {  // try_get copying out while another thread frees the job
+    CHECK(A.init(0, 16) == MTB_OK, "init");
+    const int n = 256, len = 4096;
+    const std::vector<double> s = series_of(99, len);
+    for (int r = 0; r < 40; ++r) {
+        int64_t jid = 0;
+        CHECK(A.submit(s.data(), len, n, 1, MTB_DETREND_NONE, MTB_WINDOW_NONE, 0, MTB_PREC_F32, MTB_OUT_POWER, &jid) == MTB_OK,
+              "submit");
+        std::vector<double> out((size_t)(len - n + 1) * (n / 2));
+        std::thread poller([&] {
+            int ready = 0, got = 0;
+            for (int p = 0; p < 2000; ++p) {
+                const int st = A.try_get(jid, out.data(), (int)out.size(), &got, &ready);
+                if (st == MTB_BAD_ARGS || ready) break;  // freed under us, or done
+            }
+        });
+        std::this_thread::sleep_for(std::chrono::microseconds(20 * (r % 5)));
+        CHECK(A.free_job(jid) == MTB_OK, "free");
+        poller.join();
+    }
+    A.shutdown();
+}
+
+void plan_race() {  // execute vs set_topk vs destroy on shared plans
+    const int n = 512, W = 64;
+    std::vector<double> x((size_t)W * n, 1.5), y((size_t)W * n);
+    for (int r = 0; r < 30; ++r) {
+        const int64_t p = A.plan_create(0, n, n, W, MTB_DETREND_KALMAN, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER);
+        CHECK(p > 0, "plan_create");
+        std::atomic<bool> stop{false};
+        std::thread ex([&] {
+            while (!stop) {
+                const int st = A.plan_execute(p, x.data(), y.data(), nullptr);
+                if (st == MTB_BAD_ARGS) break;  // destroyed
+            }
+        });
+        std::thread tk([&] {
+            for (int i = 0; i < 50 && !stop; ++i) A.plan_set_topk(p, 1 + i % 8, 18.0, 200.0);
+        });
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        CHECK(A.plan_destroy(p) == MTB_OK, "destroy");
+        stop = true;
+        ex.join();
+        tk.join();
+        CHECK(A.plan_destroy(p) == MTB_BAD_ARGS, "double destroy");
+    }
+}
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 2) return 2;
+    void *h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        fprintf(stderr, "dlopen: %s\n", dlerror());
+        return 3;
+    }
+    sym(h, A.init, "gpu_init");
+    sym(h, A.shutdown, "gpu_shutdown");
+    sym(h, A.fft, "gpu_fft_real_forward");
+    sym(h, A.submit, "gpu_submit_spectrum_batch");
+    sym(h, A.try_get, "gpu_try_get_spectrum_batch");
+    sym(h, A.free_job, "gpu_free_job");
+    sym(h, A.batch, "gpu_spectrum_batch");
+    sym(h, A.plan_create, "wsp_plan_create");
+    sym(h, A.plan_execute, "wsp_plan_execute");
+    sym(h, A.plan_set_topk, "wsp_plan_set_topk");
+    sym(h, A.plan_destroy, "wsp_plan_destroy");
+
+    // the session outlives every chart below; a different device is refused while it is open
+    CHECK(A.init(0, 8) == MTB_OK, "main init");
+    CHECK(A.init(-1, 8) == MTB_BAD_ARGS, "device switch while open");
+    std::atomic<int> early_done{0};
+    std::vector<std::thread> th;
+    for (int c = 0; c < 28; ++c) th.emplace_back(chart, c, c % 2 == 0, std::ref(early_done), 6);
+    th.emplace_back(free_race);
+    th.emplace_back(plan_race);
+    for (auto &t : th) t.join();
+    CHECK(early_done == 14, "early charts %d", early_done.load());
+    // main's own reference still holds the session: a sync batch works
+    const std::vector<double> s = series_of(5, 1024);
+    std::vector<double> out(8 * 64);
+    int got = 0;
+    CHECK(A.batch(s.data(), 1024, 128, 128, MTB_DETREND_MEAN, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, out.data(),
+                  (int)out.size(), &got) == MTB_OK && got == 8, "final batch");
+    CHECK(check_records(s, out.data(), 128, 128, 8, 64), "final records");
+    A.shutdown();
+    CHECK(A.init(-1, 4) == MTB_OK, "device switch after the last shutdown");
+    A.shutdown();
+    printf("hostsan stress: %s (%d failures)\n", g_fail ? "FAIL" : "ok", g_fail.load());
+    return g_fail ? 1 : 0;
+}

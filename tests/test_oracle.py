@@ -106,6 +106,36 @@ def test_kalman_tracks_a_ramp():
     assert np.max(np.abs(t[100:] - x[100:])) < 1e-3
 
 
+@pytest.mark.parametrize("kw", [{}, {"ema": 12.0}, {"adapt": 0.0}, {"clip": 0.0}, {"follow": 2.5, "iv": 1e-4, "ia": -1e-6}])
+def test_kalman_c_vs_numpy_transliteration(kw):
+    """The C oracle's StepKalman4D (wavespec_oracle.c) against the independent numpy transliteration
+    (oracle.numpy_kalman_trend, same expression order as kalman-fast.mq5:2031-2125): identical bits
+    for the defaults and four other parameter sets, over windows of every shape the tests use."""
+    names = ["follow", "qp", "qv", "qa", "qj", "adapt", "r", "vp", "vv", "va", "vj", "iv", "ia", "ij", "clip", "ema"]
+    kp = list(oracle.KALMAN_DEFAULTS)
+    for k, v in kw.items():
+        kp[names.index(k)] = v
+    n, w = 1024, 6
+    s = synth.random_walk(n * w, seed=77)
+    s[2000] += 0.05  # a jump that trips the innovation clip and the adaptive boost
+    X = s.reshape(w, n)
+    got = oracle.numpy_kalman_trend(X, kp)
+    kpa = np.asarray(kp, dtype=np.float64)
+    for i in range(w):
+        t = np.empty(n)
+        x = np.ascontiguousarray(X[i])
+        oracle.lib().ora_kalman_trend(oracle._p(x), n, oracle._p(kpa), oracle._p(t))
+        assert np.array_equal(t, got[i]), (kw, i)
+
+
+@pytest.mark.parametrize("n", [64, 1024])
+def test_kalman_spectrum_vs_numpy(n):
+    x = synth.random_walk(n, seed=n)
+    p = oracle.window_spectrum(x, "kalman", "hann", 0, kalman=oracle.KALMAN_DEFAULTS)
+    ref = oracle.numpy_spectrum(x, "kalman", "hann", 0, kalman=oracle.KALMAN_DEFAULTS)
+    assert oracle.rel_err(p, ref) < 1e-10
+
+
 def test_batch_matches_single_windows():
     s = synth.random_walk(5000, 9)
     b = oracle.batch_spectrum(s, 512, 300, "iir", "hann", 200)
