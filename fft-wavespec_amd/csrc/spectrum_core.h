@@ -141,12 +141,23 @@ template <int LOG2N> struct Geo {
 
 __device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
 __device__ __forceinline__ int pad32(int i) { return i + (i >> 5); }
-// pad16(base + STRIDE*r) written so the per-r part is a compile-time constant
+// One pad element per 2^PS: padS<4> = pad16.
+template <int PS> __device__ __forceinline__ int padS(int i) { return i + (i >> PS); }
+// padS(base + STRIDE*r) written so the per-r part is a compile-time constant
 // (folds into the ds_read/ds_write immediate offset instead of one address
-// VGPR per access): for STRIDE % 16 == 0, pad16(x + 16k) = pad16(x) + 17k.
-template <int STRIDE> __device__ __forceinline__ int pad16_at(int pbase, int base, int r) {
-    if constexpr (STRIDE % 16 == 0) return pbase + (STRIDE / 16) * 17 * r;
-    else return pad16(base + STRIDE * r);
+// VGPR per access): for STRIDE % 2^PS == 0, padS(x + STRIDE k) = padS(x) + (STRIDE + STRIDE/2^PS) k.
+template <int STRIDE, int PS = 4> __device__ __forceinline__ int pad16_at(int pbase, int base, int r) {
+    if constexpr (STRIDE % (1 << PS) == 0) return pbase + (STRIDE + (STRIDE >> PS)) * r;
+    else return padS<PS>(base + STRIDE * r);
+}
+// Pad spacing of the exchange written by pass X.  The AoS exchange (16-B elements) and the first
+// split exchange keep one pad per 16 (conflict-free 8-B writes of the radix-16 pass's lane-strided
+// outputs; its reads of 32 consecutive elements then see one 2-way conflict, as the writes would
+// under any other spacing).  The later split exchanges write runs of >= 16 consecutive elements:
+// one pad per 32 / 64 / 128 at N = 1024 / 2048 / 4096 makes both their 8-B writes and their 8-B
+// reads conflict-free (exhaustive bank simulation of every widx/ridx pattern).
+template <int LOG2N, int X, bool SPLIT> constexpr int pad_shift() {
+    return (SPLIT && X >= 1 && LOG2N >= 10 && LOG2N <= 12) ? LOG2N - 5 : 4;
 }
 
 // Window classes: none; a0 + a1 cos th + a2 cos 2th (Hann, Hamming, Blackman);
@@ -191,31 +202,31 @@ template <typename T> struct SpecArgs {
 };
 
 // LDS element index (padded) where pass PASS writes its element i = q*R + r.
-template <int LOG2N, int PASS> __device__ __forceinline__ int widx(int t, int i) {
+template <int LOG2N, int PASS, int PS = 4> __device__ __forceinline__ int widx(int t, int i) {
     using G = Geo<LOG2N>;
     constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
     const int q = i / R, r = i % R, b = t + G::TPW * q;
     if constexpr (PASS == 0) {
-        // R consecutive elements: pad16(b R + r) = pad16(b R) + r (b R % 16 + r < 16 for R | 16)
-        return pad16(b * R) + r;
+        // R consecutive elements: padS(b R + r) = padS(b R) + r (b R % 2^PS + r < 2^PS for R | 16 | 2^PS)
+        return padS<PS>(b * R) + r;
     } else {
         const int base = (b / Ns) * Ns * R + (b % Ns);
-        return pad16_at<Ns>(pad16(base), base, r);
+        return pad16_at<Ns, PS>(padS<PS>(base), base, r);
     }
 }
 
 // LDS element index pass PASS reads its element i from (the final pass owns
 // butterflies {t, B-t}, {0, B/2} for t = 0).
-template <int LOG2N, int PASS> __device__ __forceinline__ int ridx(int t, int i) {
+template <int LOG2N, int PASS, int PS = 4> __device__ __forceinline__ int ridx(int t, int i) {
     using G = Geo<LOG2N>;
     if constexpr (PASS == G::NPASS - 1) {
         const int q = i / 8, r = i % 8;
         const int b = q == 0 ? t : (t == 0 ? G::TPW : 2 * G::TPW - t);
-        return pad16_at<G::B>(pad16(b), b, r);
+        return pad16_at<G::B, PS>(padS<PS>(b), b, r);
     } else {
         constexpr int R = G::radix(PASS);
         const int q = i / R, r = i % R, b = t + G::TPW * q;
-        return pad16_at<G::M / R>(pad16(b), b, r);
+        return pad16_at<G::M / R, PS>(padS<PS>(b), b, r);
     }
 }
 
@@ -240,18 +251,19 @@ __device__ __forceinline__ void exchange(char *base, cpx<T> (&v)[16], int t) {
         using RT = std::conditional_t<SPLIT == 2, const volatile __attribute__((address_space(3))) T,
                                       const __attribute__((address_space(3))) T>;
         RT *rs = (RT *)s;  // LDS address space: the volatile view must stay a ds_read, not a flat load
+        constexpr int PS = sizeof(T) == 8 ? pad_shift<LOG2N, PASS, true>() : 4;  // 8-B elements (f64 halves)
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].re;
+        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS, PS>(t, i)] = v[i].re;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i].re = rs[ridx<LOG2N, PASS + 1>(t, i)];
+        for (int i = 0; i < 16; ++i) v[i].re = rs[ridx<LOG2N, PASS + 1, PS>(t, i)];
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS>(t, i)] = v[i].im;
+        for (int i = 0; i < 16; ++i) s[widx<LOG2N, PASS, PS>(t, i)] = v[i].im;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i].im = rs[ridx<LOG2N, PASS + 1>(t, i)];
+        for (int i = 0; i < 16; ++i) v[i].im = rs[ridx<LOG2N, PASS + 1, PS>(t, i)];
     }
 }
 

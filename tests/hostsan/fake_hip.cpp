@@ -173,6 +173,18 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
     });
     return hipSuccess;
 }
+hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int) {
+    uint64_t gen;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        gen = e->recorded;  // the most recent record at the time of the call
+    }
+    run_on(s, [e, gen] {
+        std::unique_lock<std::mutex> lk(e->mu);
+        e->cv.wait(lk, [e, gen] { return e->reached >= gen; });
+    });
+    return hipSuccess;
+}
 hipError_t hipEventQuery(hipEvent_t e) {
     std::lock_guard<std::mutex> lk(e->mu);
     return e->reached >= e->recorded ? hipSuccess : hipErrorNotReady;
