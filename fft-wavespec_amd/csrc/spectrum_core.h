@@ -154,10 +154,11 @@ template <int STRIDE, int PS = 4> __device__ __forceinline__ int pad16_at(int pb
 // split exchange keep one pad per 16 (conflict-free 8-B writes of the radix-16 pass's lane-strided
 // outputs; its reads of 32 consecutive elements then see one 2-way conflict, as the writes would
 // under any other spacing).  The later split exchanges write runs of >= 16 consecutive elements:
-// one pad per 32 / 64 / 128 at N = 1024 / 2048 / 4096 makes both their 8-B writes and their 8-B
-// reads conflict-free (exhaustive bank simulation of every widx/ridx pattern).
+// one pad per 64 / 128 at N = 2048 / 4096 makes both their 8-B writes and their 8-B reads
+// conflict-free (exhaustive bank simulation of every widx/ridx pattern; at N = 1024 one pad per 32
+// would too, but its mean-detrend instantiation then spills at 168 VGPRs).
 template <int LOG2N, int X, bool SPLIT> constexpr int pad_shift() {
-    return (SPLIT && X >= 1 && LOG2N >= 10 && LOG2N <= 12) ? LOG2N - 5 : 4;
+    return (SPLIT && X >= 1 && LOG2N >= 11 && LOG2N <= 12) ? LOG2N - 5 : 4;
 }
 
 // Window classes: none; a0 + a1 cos th + a2 cos 2th (Hann, Hamming, Blackman);
@@ -211,7 +212,13 @@ template <int LOG2N, int PASS, int PS = 4> __device__ __forceinline__ int widx(i
         return padS<PS>(b * R) + r;
     } else {
         const int base = (b / Ns) * Ns * R + (b % Ns);
-        return pad16_at<Ns, PS>(padS<PS>(base), base, r);
+        if constexpr (Ns < (1 << PS) && (Ns * R) % (1 << PS) == 0) {
+            // base mod 2^PS = b mod Ns < Ns, and Ns | 2^PS: adding Ns r crosses a multiple of 2^PS exactly
+            // at the compile-time r's where Ns r does, so the per-r part stays an immediate offset
+            return padS<PS>(base) + Ns * r + ((Ns * r) >> PS);
+        } else {
+            return pad16_at<Ns, PS>(padS<PS>(base), base, r);
+        }
     }
 }
 

@@ -346,7 +346,8 @@ int main(int argc, char **argv) {
     printf("# W=%lld N=%d algorithmic bytes=%.3f GB, roofline(8 TB/s)=%.1f us\n", (long long)W, n, bytes / 1e9,
            bytes / 8e12 * 1e6);
 
-    const int grids[] = {8192, 16384, 32768, 65536};
+    // fixed sizes and whole rounds of resident workgroups (6 per CU x 256 CUs = 1536 at 3 waves/SIMD)
+    const int grids[] = {1536, 3072, 6144, 12288, 21846, 32768, 65536};
     for (int round = 0; round < rounds; ++round) {
         // copy ceiling
         if (getenv("KBENCH_COPIES")) {
@@ -385,7 +386,8 @@ int main(int argc, char **argv) {
             struct {
                 const char *name;
                 float us;
-            } r[4] = {{"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
+            } r[5] = {{"library", time_variant<kDefaultVar | kVarNtLoad>(L, s, reps)},
+                      {"split+nt2", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore>(L, s, reps)},
                       {"split+nt2+rec+b64", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore |
                                                          kVarWinRec | kVarLdsB64>(L, s, reps)},
                       {"split+nt2+twtab", time_variant<kVarSplitLds | kVarNoPrefetch | kVarNtLoad | kVarNtStore | kVarTwTable>(L, s, reps)},

@@ -30,13 +30,27 @@ for r in rows("trace/**/*kernel_stats.csv"):
                                                           "min_us": float(r["MinNs"]) / 1e3}
 
 
+def main_per_step(cfg):
+    """Main-kernel dispatches per bench step: 1, or the chunk count of the four-step large-N path
+    (one row_kernel per chunk of windows, csrc/large_fft.hip large_chunk: 192 MiB of column results)."""
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "fft-wavespec_amd"))
+    from wavespec_amd import synth
+    c = synth.CONFIGS.get(cfg)
+    if not c or c["n"] <= 16384:
+        return 1
+    per = (c["n"] // 2) * (8 if c["precision"] == "f32" else 16)
+    chunk = max(1, (192 << 20) // per)
+    return -(-c["windows"] // chunk)
+
+
 def pmc(pattern, counter):
     """Counter bytes per step: every dispatch of our kernels summed, divided by the number of
-    main-kernel dispatches (C3's Kalman pre-pass traffic belongs to the step it feeds)."""
+    main-kernel dispatches, times the main dispatches per step (C3's Kalman pre-pass traffic belongs
+    to the step it feeds; a large-N step is several chunks)."""
     rs = [r for r in rows(pattern) if r.get("Counter_Name") == counter]
     vals = [float(r["Counter_Value"]) for r in rs if any(k in r.get("Kernel_Name", "") for k in OURS)]
     n_main = sum(1 for r in rs if any(k in r.get("Kernel_Name", "") for k in MAIN))
-    return sum(vals) / n_main if n_main else None
+    return sum(vals) / n_main * main_per_step(cfg) if n_main else None
 
 
 fetch = pmc("fetch/**/*counter_collection.csv", "FETCH_SIZE")
