@@ -424,6 +424,232 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Packed two-segment filter (fp32 plans, reference default flags: adaptive boost + clip, no EMA).
+//
+// At C3 the one-lane-per-window filter is one lone wave per SIMD, and a lone wave issues one VALU
+// instruction per 4 cycles whether it is v_fma_f32 or v_pk_fma_f32 (MI355X_MICROARCH.md, issue
+// cost): a packed instruction does two lanes' worth of filter work for the price of one.  The
+// window's own recurrence has no pair structure left to pack (kstep PKUP packs what there is), so
+// each lane runs TWO time segments of its window side by side as the halves of float2 registers:
+//   .x  segment A: ResetKalmanState at sample 0, samples [0, L0)                 (exact)
+//   .y  segment B: ResetKalmanState at sample L0 - WU, WU warm-up steps without output,
+//                  then samples [L0, N)                                           L0 = (N + WU) / 2
+// so that every step of the lane is one packed step of both (L0 steps instead of N).  The filter
+// forgets its start (a cold start contracts onto the sequential trajectory; numpy, C3 data: 4e-16
+// after 256 steps in fp64, 1-6 ulps in fp32).  The warm-up is VERIFIED per window: after its
+// last step segment A holds the exact state at sample L0 - 1, which segment B reached after its
+// warm-up (kept from then); every component must agree within 2^-16 relative plus an absolute
+// floor of 2^-24 (|x0| + |pos|) -- half an fp32 ulp of the price level, below what an fp32
+// series can resolve.  Any window that fails makes its wave re-run [L0, N) from segment A's
+// exact state (wave-uniform branch), so a filter that has not converged is never used.  The
+// outputs agree with the sequential fp32 filter to the fp32 rounding of the state (not bit for
+// bit), i.e. well inside the f32 plan's parity bar (1e-5 of the spectrum); fp64 plans keep the
+// sequential kernel.
+typedef float kf2 __attribute__((ext_vector_type(2)));
+
+struct KState2 {
+    kf2 pos, vel, acc, jerk, p00, p01, p02, p03, p11, p12, p13, p22, p23, p33;
+};
+
+__device__ __forceinline__ kf2 krsq2(kf2 s) { return kf2{__builtin_amdgcn_rsqf(s.x), __builtin_amdgcn_rsqf(s.y)}; }
+__device__ __forceinline__ kf2 kfloor2(kf2 v) { return kf2{fmaxf(1e-12f, v.x), fmaxf(1e-12f, v.y)}; }
+
+// StepKalman4D :2031-2125 for both segments: the two-stage predict and the normalised update of
+// kstep<float, true, true>, every operation a packed one except rsq / min / clamp / floor.
+__device__ __forceinline__ kf2 kstep_pk2(KState2 &st, const KConst<float> &c, kf2 z) {
+    const kf2 pos = st.pos, vel = st.vel, acc = st.acc, jerk = st.jerk;
+    const kf2 p00 = st.p00, p01 = st.p01, p02 = st.p02, p03 = st.p03, p11 = st.p11, p12 = st.p12, p13 = st.p13,
+              p22 = st.p22, p23 = st.p23, p33 = st.p33;
+    const kf2 x0p = pos + vel + 0.5f * acc + (1.0f / 6.0f) * jerk;
+    const kf2 x1p = vel + acc + 0.5f * jerk;
+    const kf2 x2p = acc + jerk;
+    const kf2 x3p = jerk;
+    const kf2 a00 = p00 + p01 + 0.5f * p02 + (1.0f / 6.0f) * p03;
+    const kf2 a01 = p01 + p11 + 0.5f * p12 + (1.0f / 6.0f) * p13;
+    const kf2 a02 = p02 + p12 + 0.5f * p22 + (1.0f / 6.0f) * p23;
+    const kf2 a03 = p03 + p13 + 0.5f * p23 + (1.0f / 6.0f) * p33;
+    const kf2 a11 = p11 + p12 + 0.5f * p13;
+    const kf2 a12 = p12 + p22 + 0.5f * p23;
+    const kf2 a13 = p13 + p23 + 0.5f * p33;
+    const kf2 a22 = p22 + p23;
+    const kf2 a23 = p23 + p33;
+    kf2 P00p = a00 + a01 + 0.5f * a02 + (1.0f / 6.0f) * a03 + c.Qp;
+    const kf2 P01p = a01 + a02 + 0.5f * a03;
+    const kf2 P02p = a02 + a03;
+    const kf2 P03p = a03;
+    kf2 P11p = a11 + 2.0f * a12 + 0.5f * (a13 + p13) + c.Qv;  // the reference's P11 (:2052), see kstep
+    const kf2 P12p = a12 + a13;
+    const kf2 P13p = a13;
+    kf2 P22p = a22 + a23 + c.Qa;
+    const kf2 P23p = a23;
+    kf2 P33p = p33 + c.Qj;
+
+    const kf2 y = z - x0p;
+    kf2 S = P00p + c.R;
+    const kf2 yr = y * krsq2(S);  // boost - 1 = min(5, |y|/sigma) g, g folded into gQ*
+    const kf2 k = {fminf(5.0f, fabsf(yr.x)), fminf(5.0f, fabsf(yr.y))};
+    P00p += k * c.gQp;
+    P11p += k * c.gQv;
+    P22p += k * c.gQa;
+    P33p += k * c.gQj;
+    S = P00p + c.R;
+    const kf2 rs = krsq2(S);
+    kf2 yn = y * rs;
+    yn = kf2{__builtin_amdgcn_fmed3f(yn.x, -c.clip, c.clip), __builtin_amdgcn_fmed3f(yn.y, -c.clip, c.clip)};
+    const kf2 g0 = P00p * rs, g1 = P01p * rs, g2 = P02p * rs, g3 = P03p * rs;
+    st.pos = x0p + g0 * yn;
+    st.vel = x1p + g1 * yn;
+    st.acc = x2p + g2 * yn;
+    st.jerk = x3p + g3 * yn;
+    st.p00 = kfloor2(P00p - g0 * g0);
+    st.p01 = P01p - g1 * g0;
+    st.p02 = P02p - g2 * g0;
+    st.p03 = P03p - g3 * g0;
+    st.p11 = kfloor2(P11p - g1 * g1);
+    st.p12 = P12p - g2 * g1;
+    st.p13 = P13p - g3 * g1;
+    st.p22 = kfloor2(P22p - g2 * g2);
+    st.p23 = P23p - g3 * g2;
+    st.p33 = kfloor2(P33p - g3 * g3);
+    return st.pos;
+}
+
+constexpr int kPk2Warm = 256;
+// can the packed two-segment kernel take windows of n samples with tiles of J steps?
+constexpr bool pk2_fits(int n, int J = 32, int WU = kPk2Warm) { return n >= 4 * WU && ((n + WU) / 2) % J == 0; }
+
+__device__ __forceinline__ bool kagree(float a, float b, float floor_) {
+    return fabsf(a - b) <= 0x1p-16f * (fabsf(a) + fabsf(b)) + floor_;
+}
+
+// WAVES independent waves per workgroup, each 64 windows (one per lane) and its own LDS tile of
+// [window][step] (A, B) pairs, row stride J + 2 pairs (68 dwords at J = 32):
+//  * global IO moves rows of J contiguous samples, 16 B per lane (8 lanes per row, 8 rows per wave
+//    instruction), through buffer descriptors based at the wave's first window; the uniform row
+//    offsets ride in soffset, the lane's offset in voffset (no address VALU per access);
+//  * a lane's 4 samples of a segment-A row and of the segment-B row of the same window and
+//    columns land as 4 (A, B) pairs = two ds_write_b128, and leave the same way;
+//  * the filter reads two steps of both segments per ds_read_b128.
+// With 68-dword rows every one of these LDS accesses is conflict-free: 16 lanes of a b128 access
+// cover the 64 banks once (rows 4 banks apart, 8 lanes of a row 8 banks apart).
+template <int J, int WAVES, int WU = kPk2Warm>
+__global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
+                                                                int64_t hop, int64_t n_windows, int n, KP kp,
+                                                                unsigned *fallbacks = nullptr) {
+    static_assert(J == 32 && WU % J == 0, "8 lanes x 4 samples per row, whole tiles of warm-up");
+    constexpr int RS = J + 2;  // row stride in pairs
+    __shared__ __attribute__((aligned(16))) kf2 tiles[WAVES][64 * RS];
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x % 64, wv = WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / 64) : 0;
+    kf2 *tile = tiles[wv];
+    const int64_t w0 = ((int64_t)blockIdx.x * WAVES + wv) * 64;
+    const KConst<float> kc = kconst<float, kKfAdapt | kKfClip>(kp);
+    const int L0 = (n + WU) / 2, seg_off = L0 - WU, nchunks = L0 / J;
+    constexpr int WUC = WU / J;
+    const int rl = l / 8, q = l % 8;  // IO: row rl of the instruction's 8, samples 4q .. 4q + 3
+    const int64_t rows = n_windows - w0 < 64 ? (n_windows > w0 ? n_windows - w0 : 0) : 64;
+    const auto rin = kbuf(series + (rows > 0 ? w0 * hop : 0), rows > 0 ? (uint32_t)(((rows - 1) * hop + n) * (int64_t)sizeof(float)) : 0u);
+    const auto rout = kbuf(dout + w0 * (int64_t)n, (uint32_t)(rows * n * (int64_t)sizeof(float)));
+    const uint32_t vin = (uint32_t)((rl * hop + 4 * q) * (int64_t)sizeof(float));
+    const uint32_t vout = (uint32_t)((rl * n + 4 * q) * (int)sizeof(float));
+    // instruction g (0..7) of segment s: rows 8 g + rl; uniform byte offsets
+    auto in_off = [&](int g, int s) { return (uint32_t)(((8 * g) * hop + s * (int64_t)seg_off) * (int64_t)sizeof(float)); };
+    auto out_off = [&](int g, int s) { return (uint32_t)(((8 * g) * (int64_t)n + s * (int64_t)seg_off) * (int64_t)sizeof(float)); };
+    auto ld4 = [&](uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)voff, (int)soff, 0));
+    };
+    auto st4 = [&](f4v v, uint32_t voff, uint32_t soff) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)voff, (int)soff, 0);
+    };
+    f4v ra[8], rb[8];
+    auto issue = [&](int c) {
+        const uint32_t vc = vin + (uint32_t)(c * J * (int)sizeof(float));
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            ra[g] = ld4(vc, in_off(g, 0));
+            rb[g] = ld4(vc, in_off(g, 1));
+        }
+    };
+    auto tpos = [&](int g) { return (8 * g + rl) * RS + 4 * q; };  // pair index of an IO lane's first sample
+
+    KState2 st;
+    float x0 = 0.f;
+    KState<float> warm;  // segment B's state after its warm-up
+    auto run = [&](int c0, int c1, int sA, int sB) {
+        issue(c0);
+        for (int c = c0; c < c1; ++c) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                f4v *t = reinterpret_cast<f4v *>(tile + tpos(g));
+                t[0] = f4v{ra[g].x, rb[g].x, ra[g].y, rb[g].y};
+                t[1] = f4v{ra[g].z, rb[g].z, ra[g].w, rb[g].w};
+            }
+            __syncthreads();
+            if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
+            if (c == 0) {
+                const kf2 f = tile[l * RS];  // (sample 0, sample L0 - WU)
+                x0 = f.x;
+                KState<float> a;
+                kreset<float>(a, kp, 0.f);
+                st.pos = kf2{0.f, f.y - x0};
+                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
+                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
+                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
+            }
+            kf2 zrow[J];
+#pragma unroll
+            for (int j = 0; j < J; j += 2) {
+                const f4v v = *reinterpret_cast<const f4v *>(tile + l * RS + j);
+                zrow[j] = kf2{v.x, v.y};
+                zrow[j + 1] = kf2{v.z, v.w};
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const kf2 z = zrow[j] - x0;  // exact for prices within 2x of x0 (Sterbenz)
+                const kf2 trend = kstep_pk2(st, kc, z);
+                zrow[j] = z - trend;
+            }
+            if (c == WUC - 1) {
+                warm.pos = st.pos.y, warm.vel = st.vel.y, warm.acc = st.acc.y, warm.jerk = st.jerk.y;
+                warm.p00 = st.p00.y, warm.p01 = st.p01.y, warm.p02 = st.p02.y, warm.p03 = st.p03.y;
+                warm.p11 = st.p11.y, warm.p12 = st.p12.y, warm.p13 = st.p13.y, warm.p22 = st.p22.y;
+                warm.p23 = st.p23.y, warm.p33 = st.p33.y;
+            }
+#pragma unroll
+            for (int j = 0; j < J; j += 2)
+                *reinterpret_cast<f4v *>(tile + l * RS + j) = f4v{zrow[j].x, zrow[j].y, zrow[j + 1].x, zrow[j + 1].y};
+            __syncthreads();
+            const uint32_t vc = vout + (uint32_t)(c * J * (int)sizeof(float));
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const f4v *t = reinterpret_cast<const f4v *>(tile + tpos(g));
+                const f4v u = t[0], v = t[1];
+                if (c >= sA) st4(f4v{u.x, u.z, v.x, v.z}, vc, out_off(g, 0));
+                if (c >= sB) st4(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1));
+            }
+            __syncthreads();
+        }
+    };
+    run(0, nchunks, 0, WUC);
+    // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it
+    const float fl = 0x1p-24f * (fabsf(x0) + fabsf(st.pos.x));
+    const bool ok = kagree(st.pos.x, warm.pos, fl) && kagree(st.vel.x, warm.vel, fl) && kagree(st.acc.x, warm.acc, fl) &&
+                    kagree(st.jerk.x, warm.jerk, fl) && kagree(st.p00.x, warm.p00, 0.f) && kagree(st.p01.x, warm.p01, 0.f) &&
+                    kagree(st.p02.x, warm.p02, 0.f) && kagree(st.p03.x, warm.p03, 0.f) && kagree(st.p11.x, warm.p11, 0.f) &&
+                    kagree(st.p12.x, warm.p12, 0.f) && kagree(st.p13.x, warm.p13, 0.f) && kagree(st.p22.x, warm.p22, 0.f) &&
+                    kagree(st.p23.x, warm.p23, 0.f) && kagree(st.p33.x, warm.p33, 0.f);
+    if (__ballot(!ok)) {  // wave-uniform: segment B's outputs [L0, N) again, from the exact state
+        if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
+        st.pos.y = st.pos.x, st.vel.y = st.vel.x, st.acc.y = st.acc.x, st.jerk.y = st.jerk.x;
+        st.p00.y = st.p00.x, st.p01.y = st.p01.x, st.p02.y = st.p02.x, st.p03.y = st.p03.x;
+        st.p11.y = st.p11.x, st.p12.y = st.p12.x, st.p13.y = st.p13.x, st.p22.y = st.p22.x;
+        st.p23.y = st.p23.x, st.p33.y = st.p33.x;
+        run(WUC, nchunks, nchunks, WUC);  // only segment B stores
+    }
+}
+
 }  // namespace kcore
 
 }  // namespace wsp

@@ -39,6 +39,17 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
     return hipGetLastError();
 }
 
+// fp32 plans with the reference default flags: two time segments per lane as packed pairs
+// (kalman_pk2_kernel).  Single-wave workgroups: at ~300 VGPRs a SIMD holds one wave of it anyway,
+// so the dispatcher cannot stack two on one SIMD, and no wave waits at another's barrier
+// (kalman_bench time, C3: 0.53-0.57 ms against 0.59-0.64 ms for 4-wave workgroups).
+hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
+    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1>), dim3((unsigned)((L.n_windows + 63) / 64)), dim3(64), 0, stream,
+                       static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp,
+                       (unsigned *)nullptr);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
@@ -47,11 +58,15 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
     static_assert(sizeof(KP) == 16 * sizeof(double), "KP layout");
     __builtin_memcpy(&kp, L.params, sizeof(kp));
     // the reference defaults (adaptive boost + clip, no EMA) run branch-free;
-    // other flag sets read them per step.  L.variant = 1 forces single-wave
-    // workgroups (ablation).
+    // other flag sets read them per step.  fp32 default-flag plans of N >= 1024
+    // run two time segments per lane (kalman_pk2_kernel).  L.variant = 1 forces
+    // single-wave workgroups, 2 the sequential fp32 filter (ablations).
     constexpr int kFixed = kcore::kKfAdapt | kcore::kKfClip;
     const bool fixed = kcore::kalman_flags(kp) == kFixed;
-    if (L.f32) return fixed ? launch_t<float, kFixed>(L, kp, stream) : launch_t<float, kcore::kKfRuntime>(L, kp, stream);
+    if (L.f32) {
+        if (fixed && L.variant == 0 && kcore::pk2_fits(L.n)) return launch_pk2(L, kp, stream);
+        return fixed ? launch_t<float, kFixed>(L, kp, stream) : launch_t<float, kcore::kKfRuntime>(L, kp, stream);
+    }
     return fixed ? launch_t<double, kFixed>(L, kp, stream) : launch_t<double, kcore::kKfRuntime>(L, kp, stream);
 }
 

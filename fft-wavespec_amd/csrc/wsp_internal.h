@@ -93,7 +93,7 @@ struct KalmanLaunch {
     int n;
     bool f32;
     double params[16];    // L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901 order
-    int variant;          // 0 auto, 1 = single-wave workgroups only (ablation)
+    int variant;          // 0 auto, 1 = single-wave workgroups only, 2 = sequential fp32 filter (ablations)
 };
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream);

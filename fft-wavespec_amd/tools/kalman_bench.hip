@@ -51,6 +51,15 @@ __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ i
         out[j] = in[j];
 }
 
+// the packed two-segment kernel (fp32, default flags)
+template <int WAVES, int WU>
+void launch_pk2(const float *x, float *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
+    const size_t stat = (size_t)WAVES * 64 * 34 * 8;
+    const size_t reserve = WAVES == 4 ? 84 * 1024 - stat : 0;
+    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, WAVES, WU>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)), dim3(64 * WAVES),
+                       reserve, s, x, d, hop, W, n, kp, g_fallbacks);
+}
+
 template <int FL, bool TWO, int WAVES, bool PK = false, int SEG = 1, int WU = kcore::kSegWarm>
 void time_variant(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n,
                   int reps, hipStream_t s) {
@@ -78,6 +87,40 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
         alt += t;
     }
     printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us\n", name, back * 1e3f / reps, alt * 1e3f / reps);
+    fflush(stdout);
+}
+
+template <int WAVES, int WU>
+void time_pk2(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n, int reps,
+              hipStream_t s) {
+    kcore::KP kp;
+    memcpy(&kp, kDefaults, sizeof(kp));
+    hipEvent_t a, b, c;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventCreate(&c));
+    CK(hipMemset(g_fallbacks, 0, 4));
+    launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+    CK(hipEventRecord(a, s));
+    for (int r = 0; r < reps; ++r) launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float back, alt = 0;
+    CK(hipEventElapsedTime(&back, a, b));
+    for (int r = 0; r < reps; ++r) {
+        hipLaunchKernelGGL(stream_copy, dim3(8192), dim3(256), 0, s, ci, co, cn);
+        CK(hipEventRecord(a, s));
+        launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+        CK(hipEventRecord(c, s));
+        CK(hipEventSynchronize(c));
+        float t;
+        CK(hipEventElapsedTime(&t, a, c));
+        alt += t;
+    }
+    unsigned fb = 0;
+    CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+    printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us   fallback waves %u of %lld x %d\n", name,
+           back * 1e3f / reps, alt * 1e3f / reps, fb, (long long)(W / 64), 1 + 2 * reps);
     fflush(stdout);
 }
 
@@ -111,6 +154,11 @@ int time_main(int reps) {
         time_variant<3, true, 4>("4-wave WG + 1 WG/CU, static, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<kcore::kKfRuntime, true, 4>("4-wave WG + 1 WG/CU, runtime, two-stage", x, d, ci, co, cn, W, n, reps, s);
         time_variant<3, true, 4, true>("4-wave WG + 1 WG/CU, static, packed update", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<4, 128>("packed 2 segments WU=128, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<4, 256>("packed 2 segments WU=256, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<4, 512>("packed 2 segments WU=512, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<1, 256>("packed 2 segments WU=256, 1-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        if (round > 0) continue;
         auto seg = [&](auto wu) {
             constexpr int WU = decltype(wu)::value;
             CK(hipMemset(g_fallbacks, 0, 4));
@@ -284,6 +332,66 @@ int check_main(int n) {
     for (int64_t w = 0; w < W; ++w) host_kalman(&xr[w * hop], n, kDefaults, &ref[w * n]);
     check_f32<false>("f32 4-wave static two-stage", xr, ref, W, hop, n);
     check_f32<true>("f32 4-wave static packed update", xr, ref, W, hop, n);
+    if (kcore::pk2_fits(n)) {  // packed two segments, against the fp64 host filter and the sequential fp32 kernel
+        kcore::KP kp;
+        memcpy(&kp, kDefaults, sizeof(kp));
+        std::vector<float> xf(xr.begin(), xr.end());
+        float *dx32, *dd32, *dq32;
+        CK(hipMalloc(&dx32, xf.size() * 4));
+        CK(hipMalloc(&dd32, W * n * 4));
+        CK(hipMalloc(&dq32, W * n * 4));
+        CK(hipMemcpy(dx32, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemset(g_fallbacks, 0, 4));
+        launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+        launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
+        CK(hipDeviceSynchronize());
+        std::vector<float> h(W * n), q(W * n);
+        CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
+        unsigned fb = 0;
+        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+        double worst = 0, scale = 0, wseq = 0;
+        int64_t same = 0;
+        for (int64_t i = 0; i < W * n; ++i) {
+            worst = fmax(worst, fabs((double)h[i] - ref[i]));
+            scale = fmax(scale, fabs(ref[i]));
+            wseq = fmax(wseq, fabs((double)h[i] - (double)q[i]));
+            same += h[i] == q[i];
+        }
+        printf("%-40s max|d-ref| / max|ref| %.3e   vs sequential fp32: max %.3e / max|ref|, %lld of %lld identical, fallback waves %u\n",
+               "f32 packed 2 segments", worst / scale, wseq / scale, (long long)same, (long long)(W * n), fb);
+        // a spike of 1000 on the second segment's cold-start sample of every third window: the
+        // warm-up check must fail there and the re-run must reproduce the sequential filter
+        std::vector<double> xs(xr);
+        const int L0 = (n + kcore::kPk2Warm) / 2;
+        for (int64_t w = 0; w < W; w += 3) xs[w * hop + L0 - kcore::kPk2Warm] += 1000.0;
+        for (auto &v : xs) v = (double)(float)v;
+        std::vector<double> refs(W * n);
+        for (int64_t w = 0; w < W; ++w) host_kalman(&xs[w * hop], n, kDefaults, &refs[w * n]);
+        std::vector<float> xsf(xs.begin(), xs.end());
+        CK(hipMemcpy(dx32, xsf.data(), xsf.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemset(g_fallbacks, 0, 4));
+        launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+        launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+        worst = scale = wseq = 0;
+        same = 0;
+        for (int64_t i = 0; i < W * n; ++i) {
+            worst = fmax(worst, fabs((double)h[i] - refs[i]));
+            scale = fmax(scale, fabs(refs[i]));
+            wseq = fmax(wseq, fabs((double)h[i] - (double)q[i]));
+            same += h[i] == q[i];
+        }
+        printf("%-40s max|d-ref| / max|ref| %.3e   vs sequential fp32: max %.3e / max|ref|, %lld of %lld identical, fallback waves %u of %lld\n",
+               "f32 packed 2 segments, spikes", worst / scale, wseq / scale, (long long)same, (long long)(W * n), fb,
+               (long long)((W + 63) / 64));
+        CK(hipFree(dx32));
+        CK(hipFree(dd32));
+        CK(hipFree(dq32));
+    }
     if (n >= 1024) {
         CK(hipMemset(g_fallbacks, 0, 4));
         check_f32<true, 2>("f32 2 segments packed update", xr, ref, W, hop, n);

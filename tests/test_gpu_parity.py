@@ -463,6 +463,47 @@ def test_kalman_ragged_and_overlap(gpu_session, prec, nwin, hop):
     assert oracle.rel_err(p, r) <= TOL[prec]
 
 
+@pytest.mark.parametrize("n,nwin,hop", [(1024, 65, 1024), (2048, 130, 2048), (4096, 63, 4096), (4096, 70, 37),
+                                        (8192, 5, 8192), (16384, 9, 16384)])
+def test_kalman_f32_two_segments(gpu_session, n, nwin, hop):
+    """fp32 Kalman at N >= 1024 with the default flags runs two time segments per lane
+    (kalman_pk2_kernel, verified warm-up): parity with the sequential oracle on ragged last tiles
+    and overlapping windows, full row and in band."""
+    s = synth.random_walk((nwin - 1) * hop + n, seed=n + nwin)
+    p = gpu(s, n, hop, "kalman", "hann", prec="f32")
+    r = ref(s.astype(np.float32).astype(np.float64), n, hop, "kalman", "hann")
+    assert p.shape == r.shape == (nwin, n // 2)
+    assert oracle.rel_err(p, r) <= TOL["f32"]
+    assert oracle.inband_err(p, r, *oracle.band(n)) <= TOL["f32"]
+
+
+@pytest.mark.parametrize("kind,at", [("spike", 0), ("spike", 128), ("jump", 0), ("jump", 200)])
+def test_kalman_f32_two_segments_fallback(gpu_session, kind, at):
+    """Disturbances around the second segment's cold start (sample L0 - WU).  A spike of 1000 on
+    that very sample is where the second segment's reset puts its level: clipped to 6 sigma per
+    step it is still far off at the hand-over, the warm-up check must fail and the wave re-run
+    [L0, N) from the exact state (unverified, those outputs would be off by orders of magnitude
+    beyond the bar).  Spikes later in the warm-up and level jumps exercise the accepted path."""
+    n, wu = 4096, 256
+    l0 = (n + wu) // 2
+    s = synth.random_walk(64 * n, seed=17)
+    for w in range(0, 64, 3):  # every third window; the others must take the fast path unharmed
+        i = w * n + l0 - wu + at
+        if kind == "spike":
+            s[i] += 1000.0
+        else:
+            s[i:(w + 1) * n] += 0.5
+    s32 = s.astype(np.float32).astype(np.float64)
+    p = gpu(s32, n, n, "kalman", "hann", prec="f32")
+    r = ref(s32, n, n, "kalman", "hann")
+    # A level jump costs the fp32 filter itself precision: the SEQUENTIAL fp32 filter, emulated in
+    # numpy float32 (oracle.numpy_kalman_trend in float32, scripts/kalman_f32_emulation.py), is at
+    # 1.72e-5 (jump at 0) and 1.36e-5 (jump at 200) on this data; the spike data stays at 2.2e-6.
+    tol = TOL["f32"] if kind == "spike" else 4e-5
+    assert oracle.rel_err(p, r) <= tol
+    assert oracle.inband_err(p, r, *oracle.band(n)) <= tol
+
+
 def _kp(**kw):
     names = ["follow", "qp", "qv", "qa", "qj", "adapt", "r", "vp", "vv", "va", "vj", "iv", "ia", "ij", "clip", "ema"]
     p = list(KALMAN)
