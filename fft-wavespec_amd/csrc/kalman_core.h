@@ -650,6 +650,185 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Four segments per window over a lane pair (fp32, default flags).  One wave per SIMD issues an
+// instruction every ~5.5 cycles whatever its form, two waves per SIMD retire a packed one every
+// ~3.6 (tools/valu_probe.hip, profiles/r02/valu_probe.log): the packed filter above is issue-bound
+// at one wave per SIMD.  Here a wave holds 32 windows: lane l < 32 runs segments 0 and 1 of window
+// l as a packed pair, lane l + 32 segments 2 and 3, so C3's 65536 windows are 2048 waves -- two per
+// SIMD at <= 256 VGPRs.  Segment k starts cold at sample k S (S = L - WU; L = (N + 3 WU)/4 steps per
+// lane), runs WU warm-up steps, then outputs [k S + WU, k S + L) (segment 0: [0, L)).  Hand-offs
+// are verified in order, each against the exact (or already verified) state of the segment
+// before it: 0 -> 1 and 2 -> 3 in-lane, 1 -> 2 across the pair (lane l -> l + 32); a failed check
+// re-runs that segment's outputs from its predecessor's final state before the next check is made.
+constexpr bool pk4_fits(int n, int J = 16, int WU = kPk2Warm) { return n >= 4 * WU && ((n + 3 * WU) / 4) % J == 0; }
+
+__device__ __forceinline__ KState<float> kget(const KState2 &s, int h) {
+    KState<float> r;
+    auto g = [h](kf2 v) { return h ? v.y : v.x; };
+    r.pos = g(s.pos), r.vel = g(s.vel), r.acc = g(s.acc), r.jerk = g(s.jerk);
+    r.p00 = g(s.p00), r.p01 = g(s.p01), r.p02 = g(s.p02), r.p03 = g(s.p03), r.p11 = g(s.p11);
+    r.p12 = g(s.p12), r.p13 = g(s.p13), r.p22 = g(s.p22), r.p23 = g(s.p23), r.p33 = g(s.p33);
+    return r;
+}
+__device__ __forceinline__ void kset(KState2 &s, int h, const KState<float> &r) {
+    auto p = [h](kf2 &v, float x) {
+        if (h) v.y = x;
+        else v.x = x;
+    };
+    p(s.pos, r.pos), p(s.vel, r.vel), p(s.acc, r.acc), p(s.jerk, r.jerk);
+    p(s.p00, r.p00), p(s.p01, r.p01), p(s.p02, r.p02), p(s.p03, r.p03), p(s.p11, r.p11);
+    p(s.p12, r.p12), p(s.p13, r.p13), p(s.p22, r.p22), p(s.p23, r.p23), p(s.p33, r.p33);
+}
+// the warm-up check of kalman_pk2_kernel: every component within 2^-16 relative, the state
+// additionally within 2^-24 (|x0| + |pos|) absolute
+__device__ __forceinline__ bool kagree_state(const KState<float> &e, const KState<float> &w, float x0) {
+    const float fl = 0x1p-24f * (fabsf(x0) + fabsf(e.pos));
+    return kagree(e.pos, w.pos, fl) && kagree(e.vel, w.vel, fl) && kagree(e.acc, w.acc, fl) && kagree(e.jerk, w.jerk, fl) &&
+           kagree(e.p00, w.p00, 0.f) && kagree(e.p01, w.p01, 0.f) && kagree(e.p02, w.p02, 0.f) && kagree(e.p03, w.p03, 0.f) &&
+           kagree(e.p11, w.p11, 0.f) && kagree(e.p12, w.p12, 0.f) && kagree(e.p13, w.p13, 0.f) && kagree(e.p22, w.p22, 0.f) &&
+           kagree(e.p23, w.p23, 0.f) && kagree(e.p33, w.p33, 0.f);
+}
+__device__ __forceinline__ KState<float> kxor32_state(const KState<float> &s) {
+    KState<float> r;
+    r.pos = kxor32(s.pos), r.vel = kxor32(s.vel), r.acc = kxor32(s.acc), r.jerk = kxor32(s.jerk);
+    r.p00 = kxor32(s.p00), r.p01 = kxor32(s.p01), r.p02 = kxor32(s.p02), r.p03 = kxor32(s.p03), r.p11 = kxor32(s.p11);
+    r.p12 = kxor32(s.p12), r.p13 = kxor32(s.p13), r.p22 = kxor32(s.p22), r.p23 = kxor32(s.p23), r.p33 = kxor32(s.p33);
+    return r;
+}
+
+// Single-wave workgroups (2 per SIMD by the 256-VGPR bound); tile and IO as kalman_pk2_kernel with
+// tile row r = lane r, at J = 16 steps per tile (the J = 32 form spills at 256 VGPRs): 4 lanes per
+// row, IO instruction g (0..3) moves tile rows 16 g .. 16 g + 15 = windows 16 (g % 2) + rl,
+// segments 2 (g / 2) and 2 (g / 2) + 1.  Row stride J + 2 = 18 pairs: the filter's ds_read_b128 /
+// ds_write_b128 (16 lanes, 16 rows) cover the 64 banks once; the IO accesses are 2-way.
+template <int J, int WU = kPk2Warm>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kalman_pk4_kernel(
+    const float *__restrict__ series, float *__restrict__ dout, int64_t hop, int64_t n_windows, int n, KP kp,
+    unsigned *fallbacks = nullptr) {
+    static_assert((J == 16 || J == 32) && WU % J == 0, "4 samples per lane, whole tiles of warm-up");
+    constexpr int RS = J + 2, LPR = J / 4, RPI = 64 / LPR, NG = 64 / RPI;  // lanes per row, rows per instruction
+    __shared__ __attribute__((aligned(16))) kf2 tile[64 * RS];
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x;
+    const bool hi = l >= 32;
+    const int64_t w0 = (int64_t)blockIdx.x * 32;
+    const KConst<float> kc = kconst<float, kKfAdapt | kKfClip>(kp);
+    const int L = (n + 3 * WU) / 4, S = L - WU, nchunks = L / J;
+    constexpr int WUC = WU / J;
+    const int rl = l / LPR, q = l % LPR;
+    const int64_t rows = n_windows - w0 < 32 ? (n_windows > w0 ? n_windows - w0 : 0) : 32;
+    const auto rin = kbuf(series + (rows > 0 ? w0 * hop : 0), rows > 0 ? (uint32_t)(((rows - 1) * hop + n) * (int64_t)sizeof(float)) : 0u);
+    const auto rout = kbuf(dout + w0 * (int64_t)n, (uint32_t)(rows * n * (int64_t)sizeof(float)));
+    const uint32_t vin = (uint32_t)((rl * hop + 4 * q) * (int64_t)sizeof(float));
+    const uint32_t vout = (uint32_t)((rl * n + 4 * q) * (int)sizeof(float));
+    // instruction g: tile rows RPI g + rl = windows RPI (g % (NG/2)) + rl, segment pair g / (NG/2)
+    auto in_off = [&](int g, int s) {
+        return (uint32_t)(((RPI * (g % (NG / 2))) * hop + (2 * (g / (NG / 2)) + s) * (int64_t)S) * (int64_t)sizeof(float));
+    };
+    auto out_off = [&](int g, int s) {
+        return (uint32_t)(((RPI * (g % (NG / 2))) * (int64_t)n + (2 * (g / (NG / 2)) + s) * (int64_t)S) * (int64_t)sizeof(float));
+    };
+    auto ld4 = [&](uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)voff, (int)soff, 0));
+    };
+    auto st4 = [&](f4v v, uint32_t voff, uint32_t soff) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)voff, (int)soff, 0);
+    };
+    f4v ra[NG], rb[NG];
+    auto issue = [&](int c) {
+        const uint32_t vc = vin + (uint32_t)(c * J * (int)sizeof(float));
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            ra[g] = ld4(vc, in_off(g, 0));
+            rb[g] = ld4(vc, in_off(g, 1));
+        }
+    };
+    auto tpos = [&](int g) { return (RPI * g + rl) * RS + 4 * q; };
+
+    KState2 st, warm2;
+    float x0 = 0.f;
+    // sm: segments whose rows this pass stores (segment k from chunk 0 if k == 0, else from WUC)
+    auto run = [&](int c0, int c1, unsigned sm) {
+        issue(c0);
+        for (int c = c0; c < c1; ++c) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                f4v *t = reinterpret_cast<f4v *>(tile + tpos(g));
+                t[0] = f4v{ra[g].x, rb[g].x, ra[g].y, rb[g].y};
+                t[1] = f4v{ra[g].z, rb[g].z, ra[g].w, rb[g].w};
+            }
+            __syncthreads();
+            if (c + 1 < c1) issue(c + 1);
+            if (c == 0) {
+                const kf2 f = tile[l * RS];  // first samples of this lane's two segments
+                const float t = kxor32(f.x);
+                x0 = hi ? t : f.x;  // window's sample 0, from lane l - 32 for the upper lanes
+                KState<float> a;
+                kreset<float>(a, kp, 0.f);
+                st.pos = f - x0;
+                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
+                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
+                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
+            }
+            kf2 zrow[J];
+#pragma unroll
+            for (int j = 0; j < J; j += 2) {
+                const f4v v = *reinterpret_cast<const f4v *>(tile + l * RS + j);
+                zrow[j] = kf2{v.x, v.y};
+                zrow[j + 1] = kf2{v.z, v.w};
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const kf2 z = zrow[j] - x0;
+                const kf2 trend = kstep_pk2(st, kc, z);
+                zrow[j] = z - trend;
+            }
+            if (c == WUC - 1) warm2 = st;
+#pragma unroll
+            for (int j = 0; j < J; j += 2)
+                *reinterpret_cast<f4v *>(tile + l * RS + j) = f4v{zrow[j].x, zrow[j].y, zrow[j + 1].x, zrow[j + 1].y};
+            __syncthreads();
+            const uint32_t vc = vout + (uint32_t)(c * J * (int)sizeof(float));
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const f4v *t = reinterpret_cast<const f4v *>(tile + tpos(g));
+                const f4v u = t[0], v = t[1];
+                const int k0 = 2 * (g / (NG / 2)), k1 = k0 + 1;
+                if ((sm >> k0 & 1) && c >= (k0 == 0 ? 0 : WUC)) st4(f4v{u.x, u.z, v.x, v.z}, vc, out_off(g, 0));
+                if ((sm >> k1 & 1) && c >= WUC) st4(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1));
+            }
+            __syncthreads();
+        }
+    };
+    run(0, nchunks, 0xfu);
+    const KState2 fin = st;
+    // 0 -> 1 (lanes < 32): segment 1's warm-up against segment 0's exact final state
+    KState<float> s1 = kget(fin, 1);
+    if (__ballot(!hi && !kagree_state(kget(fin, 0), kget(warm2, 1), x0))) {
+        if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
+        kset(st, 1, kget(fin, 0));
+        run(WUC, nchunks, 0x2u);
+        s1 = kget(st, 1);
+    }
+    // 1 -> 2 (across the pair): segment 2's warm-up (lane l + 32) against segment 1's final (lane l)
+    s1 = kxor32_state(s1);
+    KState<float> s2 = kget(fin, 0);
+    if (__ballot(hi && !kagree_state(s1, kget(warm2, 0), x0))) {
+        if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
+        kset(st, 0, s1);
+        run(WUC, nchunks, 0x4u);
+        s2 = kget(st, 0);
+    }
+    // 2 -> 3 (lanes >= 32)
+    if (__ballot(hi && !kagree_state(s2, kget(warm2, 1), x0))) {
+        if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
+        kset(st, 1, s2);
+        run(WUC, nchunks, 0x8u);
+    }
+}
+
 }  // namespace kcore
 
 }  // namespace wsp

@@ -42,7 +42,8 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
 // fp32 plans with the reference default flags: two time segments per lane as packed pairs
 // (kalman_pk2_kernel).  Single-wave workgroups: at ~300 VGPRs a SIMD holds one wave of it anyway,
 // so the dispatcher cannot stack two on one SIMD, and no wave waits at another's barrier
-// (kalman_bench time, C3: 0.53-0.57 ms against 0.59-0.64 ms for 4-wave workgroups).
+// (kalman_bench time, C3: 0.55-0.58 ms against 0.60-0.65 ms for 4-wave workgroups, 0.78-0.81 ms
+// for the four-segment lane-pair kernel at two waves per SIMD, 0.69 ms sequential).
 hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
     hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1>), dim3((unsigned)((L.n_windows + 63) / 64)), dim3(64), 0, stream,
                        static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp,

@@ -60,6 +60,11 @@ void launch_pk2(const float *x, float *d, int64_t hop, int64_t W, int n, const k
                        reserve, s, x, d, hop, W, n, kp, g_fallbacks);
 }
 
+template <int WU>
+void launch_pk4(const float *x, float *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
+    hipLaunchKernelGGL((kcore::kalman_pk4_kernel<16, WU>), dim3((W + 31) / 32), dim3(64), 0, s, x, d, hop, W, n, kp, g_fallbacks);
+}
+
 template <int FL, bool TWO, int WAVES, bool PK = false, int SEG = 1, int WU = kcore::kSegWarm>
 void time_variant(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n,
                   int reps, hipStream_t s) {
@@ -90,7 +95,7 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     fflush(stdout);
 }
 
-template <int WAVES, int WU>
+template <int WAVES, int WU, int SEGS = 2>
 void time_pk2(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n, int reps,
               hipStream_t s) {
     kcore::KP kp;
@@ -100,9 +105,13 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     CK(hipEventCreate(&b));
     CK(hipEventCreate(&c));
     CK(hipMemset(g_fallbacks, 0, 4));
-    launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+    auto go = [&]() {
+        if constexpr (SEGS == 4) launch_pk4<WU>(x, d, n, W, n, kp, s);
+        else launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+    };
+    go();
     CK(hipEventRecord(a, s));
-    for (int r = 0; r < reps; ++r) launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+    for (int r = 0; r < reps; ++r) go();
     CK(hipEventRecord(b, s));
     CK(hipEventSynchronize(b));
     float back, alt = 0;
@@ -110,7 +119,7 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     for (int r = 0; r < reps; ++r) {
         hipLaunchKernelGGL(stream_copy, dim3(8192), dim3(256), 0, s, ci, co, cn);
         CK(hipEventRecord(a, s));
-        launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+        go();
         CK(hipEventRecord(c, s));
         CK(hipEventSynchronize(c));
         float t;
@@ -122,6 +131,47 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us   fallback waves %u of %lld x %d\n", name,
            back * 1e3f / reps, alt * 1e3f / reps, fb, (long long)(W / 64), 1 + 2 * reps);
     fflush(stdout);
+}
+
+// one or two waves per SIMD?  pk2 and pk4 at half the C3 batch (pk4: one wave per SIMD) and the full one
+int occ_main(int reps) {
+    const int n = 4096;
+    const int64_t W = 65536;
+    float *x, *d;
+    CK(hipMalloc(&x, W * n * 4));
+    CK(hipMalloc(&d, W * n * 4));
+    std::vector<float> h(W * n);
+    std::mt19937_64 rng(11);
+    std::normal_distribution<double> nd;
+    double v = 1.1;
+    for (int64_t i = 0; i < W * n; ++i) {
+        v += 1e-4 * nd(rng);
+        h[i] = (float)(v + 0.002 * sin(2 * M_PI * (double)i / 50));
+    }
+    CK(hipMemcpy(x, h.data(), W * n * 4, hipMemcpyHostToDevice));
+    kcore::KP kp;
+    memcpy(&kp, kDefaults, sizeof(kp));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int round = 0; round < 2; ++round)
+        for (int64_t w : {(int64_t)16384, (int64_t)32768, (int64_t)65536}) {
+            for (int k = 0; k < 2; ++k) {
+                auto go = [&]() {
+                    if (k) launch_pk4<kcore::kPk2Warm>(x, d, n, w, n, kp, 0);
+                    else launch_pk2<1, kcore::kPk2Warm>(x, d, n, w, n, kp, 0);
+                };
+                go();
+                CK(hipEventRecord(a, 0));
+                for (int r = 0; r < reps; ++r) go();
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                printf("%s windows %6lld: %8.1f us\n", k ? "pk4" : "pk2", (long long)w, ms * 1e3f / reps);
+            }
+        }
+    return 0;
 }
 
 int time_main(int reps) {
@@ -158,6 +208,8 @@ int time_main(int reps) {
         time_pk2<4, 256>("packed 2 segments WU=256, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<4, 512>("packed 2 segments WU=512, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256>("packed 2 segments WU=256, 1-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<1, 256, 4>("packed 4 segments WU=256, lane pairs", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<1, 512, 4>("packed 4 segments WU=512, lane pairs", x, d, ci, co, cn, W, n, reps, s);
         if (round > 0) continue;
         auto seg = [&](auto wu) {
             constexpr int WU = decltype(wu)::value;
@@ -332,62 +384,56 @@ int check_main(int n) {
     for (int64_t w = 0; w < W; ++w) host_kalman(&xr[w * hop], n, kDefaults, &ref[w * n]);
     check_f32<false>("f32 4-wave static two-stage", xr, ref, W, hop, n);
     check_f32<true>("f32 4-wave static packed update", xr, ref, W, hop, n);
-    if (kcore::pk2_fits(n)) {  // packed two segments, against the fp64 host filter and the sequential fp32 kernel
+    if (kcore::pk2_fits(n)) {  // packed segments, against the fp64 host filter and the sequential fp32 kernel
         kcore::KP kp;
         memcpy(&kp, kDefaults, sizeof(kp));
-        std::vector<float> xf(xr.begin(), xr.end());
         float *dx32, *dd32, *dq32;
-        CK(hipMalloc(&dx32, xf.size() * 4));
+        CK(hipMalloc(&dx32, xr.size() * 4));
         CK(hipMalloc(&dd32, W * n * 4));
         CK(hipMalloc(&dq32, W * n * 4));
-        CK(hipMemcpy(dx32, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
-        CK(hipMemset(g_fallbacks, 0, 4));
-        launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
-        launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
-        CK(hipDeviceSynchronize());
-        std::vector<float> h(W * n), q(W * n);
-        CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
-        unsigned fb = 0;
-        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
-        double worst = 0, scale = 0, wseq = 0;
-        int64_t same = 0;
-        for (int64_t i = 0; i < W * n; ++i) {
-            worst = fmax(worst, fabs((double)h[i] - ref[i]));
-            scale = fmax(scale, fabs(ref[i]));
-            wseq = fmax(wseq, fabs((double)h[i] - (double)q[i]));
-            same += h[i] == q[i];
+        // spikes: a value of 1000 added on the cold-start sample of the given segment starts (every third window)
+        auto check_pk = [&](const char *name, int segs, std::vector<int> spikes) {
+            std::vector<double> xs(xr);
+            for (int64_t w = 0; w < W; w += 3)
+                for (int at : spikes) xs[w * hop + at] += 1000.0;
+            for (auto &v : xs) v = (double)(float)v;
+            std::vector<double> refs(W * n);
+            for (int64_t w = 0; w < W; ++w) host_kalman(&xs[w * hop], n, kDefaults, &refs[w * n]);
+            std::vector<float> xsf(xs.begin(), xs.end());
+            CK(hipMemcpy(dx32, xsf.data(), xsf.size() * 4, hipMemcpyHostToDevice));
+            CK(hipMemset(g_fallbacks, 0, 4));
+            if (segs == 4) launch_pk4<kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+            else launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+            launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
+            CK(hipDeviceSynchronize());
+            std::vector<float> h(W * n), q(W * n);
+            CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
+            unsigned fb = 0;
+            CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+            double worst = 0, scale = 0, wseq = 0, wseqv = 0;
+            int64_t same = 0;
+            for (int64_t i = 0; i < W * n; ++i) {
+                worst = fmax(worst, fabs((double)h[i] - refs[i]));
+                scale = fmax(scale, fabs(refs[i]));
+                wseq = fmax(wseq, fabs((double)h[i] - (double)q[i]));
+                wseqv = fmax(wseqv, fabs((double)q[i] - refs[i]));
+                same += h[i] == q[i];
+            }
+            printf("%-36s max|d-ref|/max|ref| %.3e (sequential fp32 %.3e)  vs sequential: %.3e, %lld of %lld identical; fallback re-runs %u\n",
+                   name, worst / scale, wseqv / scale, wseq / scale, (long long)same, (long long)(W * n), fb);
+        };
+        const int L0 = (n + kcore::kPk2Warm) / 2, WU = kcore::kPk2Warm;
+        check_pk("f32 packed 2 segments", 2, {});
+        check_pk("f32 packed 2 segments, spikes", 2, {L0 - WU});
+        if (kcore::pk4_fits(n)) {
+            const int S = (n + 3 * WU) / 4 - WU;
+            check_pk("f32 packed 4 segments", 4, {});
+            check_pk("f32 packed 4 segments, spikes at 1", 4, {S});
+            check_pk("f32 packed 4 segments, spikes at 2", 4, {2 * S});
+            check_pk("f32 packed 4 segments, spikes at 3", 4, {3 * S});
+            check_pk("f32 packed 4 segments, spikes at 1,2,3", 4, {S, 2 * S, 3 * S});
         }
-        printf("%-40s max|d-ref| / max|ref| %.3e   vs sequential fp32: max %.3e / max|ref|, %lld of %lld identical, fallback waves %u\n",
-               "f32 packed 2 segments", worst / scale, wseq / scale, (long long)same, (long long)(W * n), fb);
-        // a spike of 1000 on the second segment's cold-start sample of every third window: the
-        // warm-up check must fail there and the re-run must reproduce the sequential filter
-        std::vector<double> xs(xr);
-        const int L0 = (n + kcore::kPk2Warm) / 2;
-        for (int64_t w = 0; w < W; w += 3) xs[w * hop + L0 - kcore::kPk2Warm] += 1000.0;
-        for (auto &v : xs) v = (double)(float)v;
-        std::vector<double> refs(W * n);
-        for (int64_t w = 0; w < W; ++w) host_kalman(&xs[w * hop], n, kDefaults, &refs[w * n]);
-        std::vector<float> xsf(xs.begin(), xs.end());
-        CK(hipMemcpy(dx32, xsf.data(), xsf.size() * 4, hipMemcpyHostToDevice));
-        CK(hipMemset(g_fallbacks, 0, 4));
-        launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
-        launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
-        CK(hipDeviceSynchronize());
-        CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
-        worst = scale = wseq = 0;
-        same = 0;
-        for (int64_t i = 0; i < W * n; ++i) {
-            worst = fmax(worst, fabs((double)h[i] - refs[i]));
-            scale = fmax(scale, fabs(refs[i]));
-            wseq = fmax(wseq, fabs((double)h[i] - (double)q[i]));
-            same += h[i] == q[i];
-        }
-        printf("%-40s max|d-ref| / max|ref| %.3e   vs sequential fp32: max %.3e / max|ref|, %lld of %lld identical, fallback waves %u of %lld\n",
-               "f32 packed 2 segments, spikes", worst / scale, wseq / scale, (long long)same, (long long)(W * n), fb,
-               (long long)((W + 63) / 64));
         CK(hipFree(dx32));
         CK(hipFree(dd32));
         CK(hipFree(dq32));
@@ -409,5 +455,6 @@ int main(int argc, char **argv) {
     CK(hipMemset(g_fallbacks, 0, 4));
     CK(hipMalloc(&g_dbg, 65536 * 28 * 8));
     if (mode == "check") return check_main(argc > 2 ? atoi(argv[2]) : 256);
+    if (mode == "occ") return occ_main(argc > 2 ? atoi(argv[2]) : 10);
     return time_main(argc > 2 ? atoi(argv[2]) : 10);
 }

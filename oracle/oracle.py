@@ -158,32 +158,36 @@ def batch_topk_phase(series, n, hop, detrend="none", window="hann", trend_period
 
 
 # ---------------------------------------------------------------- numpy cross-check
-def numpy_kalman_trend(X, params=None) -> np.ndarray:
+def numpy_kalman_trend(X, params=None, dtype=np.float64) -> np.ndarray:
     """Second, independent transliteration of ResetKalmanState / StepKalman4D
     (L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:2015-2029 / :2031-2125), vectorised over windows:
     X is (W, n) or (n,); every window is reset with its first sample and stepped over all of its
     samples (the per-window discipline of wavespec_oracle.c ora_kalman_trend).  Expression order
     follows the MQL5 source statement by statement, including the full 16-entry covariance and
-    the P11 prediction of :2052; shares no code with the C oracle."""
+    the P11 prediction of :2052; shares no code with the C oracle.
+
+    dtype=np.float32 runs the same statements in float32 (numpy keeps float32 arrays float32
+    against Python-float constants): an emulation of a SEQUENTIAL fp32 filter, used to bound
+    what fp32 arithmetic itself costs on a given input (tests of the device's fp32 filter)."""
     kp = KALMAN_DEFAULTS if params is None else list(params)
     (follow, q_pos, q_vel, q_acc, q_jerk, adapt_gain, meas_noise, var_pos, var_vel, var_acc, var_jerk, init_vel,
      init_acc, init_jerk, clip_std, ema_period) = [float(v) for v in kp]
-    X = np.asarray(X, dtype=np.float64)
+    X = np.asarray(X, dtype=dtype)
     one = X.ndim == 1
     X = np.atleast_2d(X)
     W, n = X.shape
     # ResetKalmanState(first_meas) :2015-2029
-    pos, vel = X[:, 0].copy(), np.full(W, init_vel)
-    acc, jerk = np.full(W, init_acc), np.full(W, init_jerk)
-    P = np.zeros((W, 4, 4))
+    pos, vel = X[:, 0].copy(), np.full(W, init_vel, dtype=dtype)
+    acc, jerk = np.full(W, init_acc, dtype=dtype), np.full(W, init_jerk, dtype=dtype)
+    P = np.zeros((W, 4, 4), dtype=dtype)
     P[:, 0, 0], P[:, 1, 1] = max(1e-9, var_pos), max(1e-9, var_vel)
     P[:, 2, 2], P[:, 3, 3] = max(1e-9, var_acc), max(1e-9, var_jerk)
-    ema_ready, ema_prev = False, np.zeros(W)
+    ema_ready, ema_prev = False, np.zeros(W, dtype=dtype)
     q_scale = max(0.05, follow)
     Qp, Qv = max(1e-9, q_pos * q_scale), max(1e-9, q_vel * q_scale)
     Qa, Qj = max(1e-9, q_acc * q_scale), max(1e-9, q_jerk * q_scale)
     R = max(1e-9, meas_noise)
-    trend = np.empty((W, n))
+    trend = np.empty((W, n), dtype=dtype)
     g = lambda i, j: P[:, i, j]  # noqa: E731
     for t in range(n):
         z = X[:, t]

@@ -6,6 +6,7 @@ All calls go through the C ABI.
 """
 import ctypes as C
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -477,31 +478,43 @@ def test_kalman_f32_two_segments(gpu_session, n, nwin, hop):
     assert oracle.inband_err(p, r, *oracle.band(n)) <= TOL["f32"]
 
 
-@pytest.mark.parametrize("kind,at", [("spike", 0), ("spike", 128), ("jump", 0), ("jump", 200)])
-def test_kalman_f32_two_segments_fallback(gpu_session, kind, at):
-    """Disturbances around the second segment's cold start (sample L0 - WU).  A spike of 1000 on
-    that very sample is where the second segment's reset puts its level: clipped to 6 sigma per
-    step it is still far off at the hand-over, the warm-up check must fail and the wave re-run
-    [L0, N) from the exact state (unverified, those outputs would be off by orders of magnitude
-    beyond the bar).  Spikes later in the warm-up and level jumps exercise the accepted path."""
+@pytest.mark.parametrize("kind,seg,at", [("spike", (1,), 0), ("spike", (2,), 0), ("spike", (3,), 0), ("spike", (1, 2, 3), 0),
+                                         ("spike", (2,), 128), ("jump", (2,), 0), ("jump", (1,), 200)])
+def test_kalman_f32_segments_fallback(gpu_session, kind, seg, at):
+    """fp32 Kalman runs time segments that start cold and are verified at the hand-over: the
+    library's two-segment kernel (kalman_pk2_kernel) starts its second segment at L0 - WU = 2 S,
+    the four-segment ablation (kalman_pk4_kernel) segment k at k S, S = (N + 3 WU)/4 - WU.  A spike of 1000 on a segment's cold-start sample is
+    where that segment's reset puts its level: clipped to 6 sigma per step it is still far off
+    at the hand-over, so the check against the previous segment's final state must fail and the
+    segment be re-run from that state -- for the hand-over across the lane pair (segment 2) and
+    for a chain of failures (1, 2, 3) alike.  Unverified, those outputs would be orders of
+    magnitude beyond the bar.  Spikes later in the warm-up and level jumps exercise the accepted
+    path."""
     n, wu = 4096, 256
-    l0 = (n + wu) // 2
+    S = (n + 3 * wu) // 4 - wu
     s = synth.random_walk(64 * n, seed=17)
     for w in range(0, 64, 3):  # every third window; the others must take the fast path unharmed
-        i = w * n + l0 - wu + at
-        if kind == "spike":
-            s[i] += 1000.0
-        else:
-            s[i:(w + 1) * n] += 0.5
+        for k in seg:
+            i = w * n + k * S + at
+            if kind == "spike":
+                s[i] += 1000.0
+            else:
+                s[i:(w + 1) * n] += 0.5
     s32 = s.astype(np.float32).astype(np.float64)
     p = gpu(s32, n, n, "kalman", "hann", prec="f32")
     r = ref(s32, n, n, "kalman", "hann")
-    # A level jump costs the fp32 filter itself precision: the SEQUENTIAL fp32 filter, emulated in
-    # numpy float32 (oracle.numpy_kalman_trend in float32, scripts/kalman_f32_emulation.py), is at
-    # 1.72e-5 (jump at 0) and 1.36e-5 (jump at 200) on this data; the spike data stays at 2.2e-6.
-    tol = TOL["f32"] if kind == "spike" else 4e-5
+    # A level jump costs fp32 arithmetic itself precision: a SEQUENTIAL fp32 filter (the oracle's
+    # numpy transliteration run in float32, scripts/kalman_f32_emulation.py) reaches 1.7e-5 -
+    # 3.4e-5 on jump data of this kind (2.2e-6 on the spike data).  Bar: the usual 1e-5, or twice
+    # what that sequential fp32 filter itself gets on this input, whichever is larger.
+    tol = tol_in = TOL["f32"]
+    if kind == "jump":
+        sys.path.insert(0, str(ROOT / "scripts"))
+        from kalman_f32_emulation import f32_filter_err
+        e_row, e_band = f32_filter_err(s32, n)
+        tol, tol_in = max(tol, 2 * e_row), max(tol, 2 * e_band)
     assert oracle.rel_err(p, r) <= tol
-    assert oracle.inband_err(p, r, *oracle.band(n)) <= tol
+    assert oracle.inband_err(p, r, *oracle.band(n)) <= tol_in
 
 
 def _kp(**kw):
