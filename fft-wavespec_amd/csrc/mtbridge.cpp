@@ -477,11 +477,34 @@ struct LiveCtx {
     }
 };
 
+// Caller buffers page-locked by gpu_register_host (north star: "FeedCache.mqh rewired to stage
+// price bars into pinned host buffers for hipMemcpyAsync").  A registered fp64 series is DMA'd to
+// the device from where it lies, and a registered output array receives the D2H copy directly:
+// no staging copy on either side of a synchronous batch.  Held by the session, released with it.
+struct HostRegistry {
+    std::mutex mu;
+    std::map<uintptr_t, size_t> regions;  // base -> bytes, disjoint
+    // is [p, p + bytes) inside one registered region?
+    bool covers(const void *p, size_t bytes) {
+        if (!p || !bytes) return false;
+        const uintptr_t a = (uintptr_t)p;
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = regions.upper_bound(a);
+        if (it == regions.begin()) return false;
+        --it;
+        return a >= it->first && a + bytes <= it->first + it->second;
+    }
+    ~HostRegistry() {
+        for (auto &r : regions) (void)hipHostUnregister((void *)r.first);
+    }
+};
+
 struct Session {
     int device_index = 0;
     std::vector<std::unique_ptr<DeviceCtx>> devs;
     std::mutex live_mu;
     std::vector<std::unique_ptr<LiveCtx>> live_free;
+    HostRegistry host_regs;  // destroyed before devs (declared after): unregistered while the contexts live
 };
 
 // Session lifetime (SURVEY 8b "per-session refcount"): every successful
@@ -518,8 +541,9 @@ struct Batch {
     Config cfg;
     double kalman[16];
     std::vector<Part> parts;
-    void *h_in = nullptr, *h_out = nullptr;
+    void *h_in = nullptr, *h_out = nullptr;  // pinned staging (null when the caller's buffer is registered)
     size_t h_in_bytes = 0, h_out_bytes = 0;
+    double *direct_out = nullptr;            // registered caller output receiving the D2H copies
     int status = MTB_OK;
     std::string error;
     ~Batch() {
@@ -582,7 +606,11 @@ void stage_out(double *dst, const void *src, int64_t n, bool f32) {  // pinned r
 // device's streams, so that the host staging of chunk i+1, the H2D copy, the
 // kernels and the D2H copy of earlier chunks overlap.  Each part copies its
 // own input slice (with the N - hop halo of overlapping windows).
-int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out) {
+// `out_direct` (synchronous calls only): the caller's output array, used as the D2H destination
+// when it is registered, holds every record and the plan is fp64; the series likewise goes
+// straight from a registered buffer (fp32 plans convert, so they always stage).
+int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out,
+                double *out_direct = nullptr) {
     auto b = std::make_unique<Batch>();
     b->cfg = c;
     {
@@ -591,11 +619,17 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
     }
     const size_t es = c.elem();
     const int64_t in_elems = c.series_elems();
-    b->h_in_bytes = (size_t)in_elems * es;
-    b->h_out_bytes = (size_t)(c.n_windows * c.record()) * es;
-    b->h_in = host_alloc(b->h_in_bytes);
-    b->h_out = host_alloc(b->h_out_bytes);
-    if (!b->h_in || !b->h_out) return MTB_NO_MEM;
+    const size_t in_bytes = (size_t)in_elems * es, out_bytes = (size_t)(c.n_windows * c.record()) * es;
+    const bool din = !c.f32 && S.host_regs.covers(series, in_bytes);
+    if (!c.f32 && out_direct && S.host_regs.covers(out_direct, out_bytes)) b->direct_out = out_direct;
+    if (!din) {
+        b->h_in_bytes = in_bytes;
+        if (!(b->h_in = host_alloc(in_bytes))) return MTB_NO_MEM;
+    }
+    if (!b->direct_out) {
+        b->h_out_bytes = out_bytes;
+        if (!(b->h_out = host_alloc(out_bytes))) return MTB_NO_MEM;
+    }
     const int G = (int)std::min<int64_t>((int64_t)S.devs.size(), c.n_windows);
     const int64_t per_dev = (c.n_windows + G - 1) / G;
     const int64_t dev_bytes = std::max<int64_t>(1, (per_dev - 1) * c.hop + c.n) * (int64_t)es;
@@ -626,15 +660,16 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             P.done = event_alloc(P.dev);
             if (!P.done) return MTB_INTERNAL_ERROR;
             const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
-            if (e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
+            if (!din && e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
                 stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
                 staged = e1;
             }
-            const char *src = (const char *)b->h_in + (size_t)e0 * es;
+            const char *src = din ? (const char *)(series + e0) : (const char *)b->h_in + (size_t)e0 * es;
             HIP_OR(hipMemcpyAsync(P.d_in, src, P.in_bytes, hipMemcpyHostToDevice, P.stream), MTB_INTERNAL_ERROR);
             int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
             if (st != MTB_OK) return st;
-            char *dst = (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
+            char *dst = b->direct_out ? (char *)(b->direct_out + P.w0 * c.record())
+                                      : (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
             HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
             HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
             P.recorded = true;
@@ -676,6 +711,7 @@ int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int3
             const int st = part_poll(p, true);
             if (st != MTB_OK) return st;
         }
+        if (b.direct_out) continue;  // the D2H copies already landed in the caller's registered array
         const int64_t r1 = std::min<int64_t>(p.w0 + p.nw, nrec);
         stage_out(out + p.w0 * rec, (const char *)b.h_out + (size_t)(p.w0 * rec) * b.cfg.elem(), (r1 - p.w0) * rec,
                   b.cfg.f32);
@@ -691,7 +727,8 @@ int run_sync(const Config &c, const double *series, double *out, int64_t out_cap
         return MTB_BACKEND_UNAVAILABLE;
     }
     std::unique_ptr<Batch> b;
-    int st = batch_start(*S, c, series, &b);
+    const bool whole = out_cap >= c.n_windows * c.record();  // a truncated request never lands directly
+    int st = batch_start(*S, c, series, &b, whole ? out : nullptr);
     if (st != MTB_OK) return st;
     int32_t n = 0;
     st = batch_copy_out(*b, out, out_cap, true, &n);
@@ -891,6 +928,58 @@ MTB_API void gpu_shutdown(void) {
     } else if (mine) {
         release_jobs(false, me);
     }
+}
+
+MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
+    if (!ptr || count <= 0) {
+        set_error("gpu_register_host: null buffer or count %lld <= 0", (long long)count);
+        return MTB_BAD_ARGS;
+    }
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    const uintptr_t a = (uintptr_t)ptr;
+    const size_t bytes = (size_t)count * sizeof(double);
+    HostRegistry &R = S->host_regs;
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.regions.lower_bound(a);
+    const bool overlaps = (it != R.regions.end() && it->first < a + bytes) ||
+                          (it != R.regions.begin() && std::prev(it)->first + std::prev(it)->second > a);
+    if (overlaps) {
+        set_error("gpu_register_host: [%p, +%zu B) overlaps a registered buffer", (const void *)ptr, bytes);
+        return MTB_BAD_ARGS;
+    }
+    const hipError_t e = hipHostRegister(const_cast<double *>(ptr), bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        set_error("hipHostRegister(%zu bytes): %s", bytes, hipGetErrorString(e));
+        return MTB_INTERNAL_ERROR;
+    }
+    R.regions.emplace(a, bytes);
+    return MTB_OK;
+}
+
+MTB_API int32_t gpu_unregister_host(const double *ptr) {
+    auto S = session();
+    if (!S) {
+        set_error("gpu_init has not succeeded (no GPU session)");
+        return MTB_BACKEND_UNAVAILABLE;
+    }
+    HostRegistry &R = S->host_regs;
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.regions.find((uintptr_t)ptr);
+    if (!ptr || it == R.regions.end()) {
+        set_error("gpu_unregister_host: %p is not the start of a registered buffer", (const void *)ptr);
+        return MTB_BAD_ARGS;
+    }
+    const hipError_t e = hipHostUnregister(const_cast<double *>(ptr));
+    R.regions.erase(it);
+    if (e != hipSuccess) {
+        set_error("hipHostUnregister: %s", hipGetErrorString(e));
+        return MTB_INTERNAL_ERROR;
+    }
+    return MTB_OK;
 }
 
 MTB_API int32_t gpu_fft_real_forward(const double *in, int32_t len, double *out) {

@@ -59,6 +59,8 @@ SIGNATURES = {
                                               C.c_int32, C.c_int32, C.c_int32, _i64p]),
     "gpu_try_get_spectrum_batch": (C.c_int32, [C.c_int64, _d, C.c_int32, _i32p, _i32p]),
     "gpu_set_kalman_params": (C.c_int32, [_d, C.c_int32]),
+    "gpu_register_host": (C.c_int32, [_d, C.c_int64]),
+    "gpu_unregister_host": (C.c_int32, [_d]),
     "gpu_spectrum_topk_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                             C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32, _i32p]),
     "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
@@ -169,15 +171,22 @@ def _record(window_len: int, output: str, top_k: int = 8) -> int:
 
 
 def spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none", window="hann",
-                   trend_period: int = 0, precision="f64", output="power", max_records: int | None = None
-                   ) -> np.ndarray:
-    """gpu_spectrum_batch over a chronological series -> (nwin, record) array."""
+                   trend_period: int = 0, precision="f64", output="power", max_records: int | None = None,
+                   out: np.ndarray | None = None) -> np.ndarray:
+    """gpu_spectrum_batch over a chronological series -> (nwin, record) array.  `out`: a
+    caller-owned C-contiguous float64 array of at least nwin * record elements (e.g. one
+    registered with register_host, which the library then fills by DMA directly)."""
     s = np.ascontiguousarray(series, dtype=np.float64)
     nwin = 1 + (s.size - window_len) // hop
     rec = _record(window_len, output)
     if max_records is not None:
         nwin = min(nwin, max_records)
-    out = np.empty((nwin, rec), dtype=np.float64)
+    if out is None:
+        out = np.empty((nwin, rec), dtype=np.float64)
+    elif out.dtype != np.float64 or not out.flags.c_contiguous or out.size < nwin * rec:
+        raise ValueError("out must be a C-contiguous float64 array of >= nwin * record elements")
+    else:
+        out = out.reshape(-1)[: nwin * rec].reshape(nwin, rec)
     n_out = C.c_int32(0)
     _check("gpu_spectrum_batch",
            lib().gpu_spectrum_batch(_dptr(s), s.size, window_len, hop, DETREND[detrend], WINDOW[window],
@@ -236,6 +245,18 @@ def try_get_spectrum_batch(job_id: int, out: np.ndarray):
 
 def free_job(job_id: int) -> int:
     return lib().gpu_free_job(job_id)
+
+
+def register_host(a: np.ndarray) -> None:
+    """gpu_register_host: page-lock a C-contiguous float64 array for the session (FeedCache
+    history, output arrays); synchronous batch calls then DMA straight from / into it."""
+    if a.dtype != np.float64 or not a.flags.c_contiguous:
+        raise ValueError("register_host needs a C-contiguous float64 array")
+    _check("gpu_register_host", lib().gpu_register_host(_dptr(a), a.size))
+
+
+def unregister_host(a: np.ndarray) -> None:
+    _check("gpu_unregister_host", lib().gpu_unregister_host(_dptr(a)))
 
 
 def set_kalman_params(params) -> None:

@@ -4,8 +4,9 @@ Same names, argument meaning and error behaviour as the MQL5 code that calls
 ``mt-bridge.dll``; the arithmetic happens in libmtbridge.so (HIP, gfx950).
 
 * :class:`FeedCache` / :func:`ensure_feed_cache` -- Include/FeedCache.mqh:68-163
-  (file format: int32 count + doubles, newest first), staged for the device
-  by the library's pinned buffers.
+  (file format: int32 count + doubles, newest first); :func:`pin_feed_cache`
+  keeps the history page-locked (gpu_register_host) so the batch path DMAs it
+  in place -- the north star's "FeedCache rewired to pinned buffers".
 * :class:`FeedBuilder` -- FeedBuilder::Build / BuildPlaPriceSeries (1.1.0:474-506, 760-771).
 * :class:`FftProcessor` -- EnsureGpu + FftProcessor::Run (1.1.0:511-533, 722-757).
 * :func:`on_calculate` -- the per-bar OnCalculate loop restricted to the
@@ -36,12 +37,19 @@ def feed_cache_file_name(prefix: str, symbol: str, tf: str) -> str:
 
 @dataclass
 class FeedCache:
-    """struct FeedCache, Include/FeedCache.mqh:68-75 (close[] newest first)."""
+    """struct FeedCache, Include/FeedCache.mqh:68-75 (close[] newest first).
+
+    ``chrono`` is the same history oldest first in one contiguous float64 buffer: the physical
+    memory of the MQL as-series close[] array, which is what the terminal hands the DLL.  Once
+    :func:`pin_feed_cache` has registered it, ``pinned`` is True and ensure_feed_cache keeps the
+    registration on the current buffer as the history grows."""
     symbol: str = ""
     tf: str = ""
     close: np.ndarray = field(default_factory=lambda: np.empty(0))
     loaded: bool = False
     from_file: bool = False
+    chrono: np.ndarray = field(default_factory=lambda: np.empty(0))
+    pinned: bool = False
 
 
 def save_feed_cache(path: str, close_newest_first: np.ndarray) -> None:
@@ -99,7 +107,37 @@ def ensure_feed_cache(cache: FeedCache, symbol: str, tf: str, needed_bars: int, 
     cache.loaded = cached > 0
     if enable_cache and cache.loaded:
         save_feed_cache(path, cache.close)
+    if cache.chrono.size != cache.close.size or (cache.close.size and cache.chrono[-1] != cache.close[0]):
+        _restage(cache)
     return cached >= needed_bars, delta_added, from_file
+
+
+def _restage(cache: FeedCache) -> None:
+    """Rebuild the chronological buffer after the history changed (ArrayResize in MQL moves the
+    array: the old registration is dropped and the new buffer registered)."""
+    was = cache.pinned
+    if was:
+        unpin_feed_cache(cache)
+    cache.chrono = np.ascontiguousarray(cache.close[::-1], dtype=np.float64)
+    if was:
+        pin_feed_cache(cache)
+
+
+def pin_feed_cache(cache: FeedCache) -> None:
+    """Page-lock the feed history for the device (gpu_register_host, needs an open session):
+    synchronous batch calls on ``cache.chrono`` then DMA it in place instead of copying it
+    through the library's staging buffers (include/mtbridge.h, "Pinned feed staging")."""
+    if cache.chrono.size != cache.close.size:
+        cache.chrono = np.ascontiguousarray(cache.close[::-1], dtype=np.float64)
+    if cache.chrono.size and not cache.pinned:
+        bridge.register_host(cache.chrono)
+        cache.pinned = True
+
+
+def unpin_feed_cache(cache: FeedCache) -> None:
+    if cache.pinned:
+        cache.pinned = False
+        bridge.unregister_host(cache.chrono)
 
 
 class FeedBuilder:
@@ -195,6 +233,15 @@ def on_calculate(cache: FeedCache, fft_window: int, bars: int, fft: FftProcessor
         if own:
             fft.shutdown()  # OnDeinit (1.1.0:710-716): drops this chart's reference on the session
     return out
+
+
+def feed_spectra(cache: FeedCache, fft_window: int, hop: int = 1, detrend="none", window="hann",
+                 trend_period: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    """Synchronous spectra of every window of the feed history (gpu_spectrum_batch on
+    ``cache.chrono``): with the cache pinned and ``out`` registered, the input and the results
+    cross PCIe by DMA only (fp64)."""
+    return bridge.spectrum_batch(cache.chrono, fft_window, hop, detrend, window, trend_period, "f64", "power",
+                                 out=out)
 
 
 def batch_spectra(prices: np.ndarray, fft_window: int, hop: int = 1, detrend="none", window="hann",

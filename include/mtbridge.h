@@ -209,6 +209,25 @@ MTB_API int32_t gpu_spectrum_topk_phase_batch(const double *series, int32_t seri
  * clip_std, ema_blend_period.  n must be 16.  Process-wide. */
 MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
 
+/* Pinned feed staging (north star: "FeedCache.mqh rewired to stage price bars
+ * into pinned host buffers for hipMemcpyAsync").  Replaces the FeedCache
+ * close-history array's plain host memory (Include/FeedCache.mqh:84-114,
+ * `struct FeedCache`) as the staging area: the caller page-locks the array it
+ * already keeps (hipHostRegister, portable across the session's devices) after
+ * each ArrayResize, and the synchronous batch calls (gpu_spectrum_batch, the
+ * top-k variants, gpu_fft_real_forward_batch) then DMA an fp64 series straight
+ * from it and write a whole fp64 result straight into a registered output
+ * array -- no copy through the library's own staging buffers.  fp32 plans
+ * convert and truncated outputs (out_cap below all records) still stage;
+ * gpu_submit_spectrum_batch still copies its input (1.1.0:1316).
+ * Registrations belong to the session and end with it (last gpu_shutdown).
+ * The caller must not unregister or free a buffer while a call reading it
+ * runs.  MTB_OK; MTB_BAD_ARGS for null/empty or overlapping ranges (register)
+ * or an unknown base pointer (unregister); MTB_BACKEND_UNAVAILABLE without a
+ * session; MTB_INTERNAL_ERROR when the runtime refuses. */
+MTB_API int32_t gpu_register_host(const double *ptr, int64_t count);
+MTB_API int32_t gpu_unregister_host(const double *ptr);
+
 /* =====================================================================
  * 4. Device-resident plans: the same hot path on buffers already in HBM
  *    (multi-GPU shards, benchmarks, pipelines that keep data on device).

@@ -13,7 +13,7 @@ import sys
 from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
-OURS = ("spectrum_kernel", "kalman_detrend_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
+OURS = ("spectrum_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
         "iir_kernel")
 MAIN = ("spectrum_kernel", "inverse_kernel", "row_kernel")  # one per step; a Kalman pre-pass adds to its step
 

@@ -1,6 +1,9 @@
 """PCIe-inclusive rate of the north-star batch through the host-buffer entry
 point gpu_spectrum_batch (pinned staging + H2D + kernel + D2H + copy-out),
-for DESIGN.md sec. 5 -- never bench.py's `value`."""
+for DESIGN.md sec. 5 -- never bench.py's `value`.
+  python3 scripts/pcie_rate.py [config] [--registered]
+--registered: the series and the output array are registered first
+(gpu_register_host, the pinned FeedCache): DMA in place, no staging copies."""
 import json
 import sys
 import time
@@ -12,21 +15,31 @@ import numpy as np  # noqa: E402
 
 from wavespec_amd import bridge, synth  # noqa: E402
 
-cfg = synth.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "north_star"]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+registered = "--registered" in sys.argv
+cfg = synth.CONFIGS[args[0] if args else "north_star"]
 n, hop, w = cfg["n"], cfg["hop"], cfg["windows"]
 s = synth.random_walk((w - 1) * hop + n, seed=cfg["seed"])
 out = np.empty((w, n // 2))
 bridge.init(0, 16)
 try:
+    if registered:
+        t0 = time.perf_counter()
+        bridge.register_host(s)
+        bridge.register_host(out)
+        t_reg = time.perf_counter() - t0
     bridge.spectrum_batch(s[: 64 * hop + n], n, hop, cfg["detrend"], cfg["window"], 0, cfg["precision"])  # warm
     ts = []
     for _ in range(3):
         t0 = time.perf_counter()
-        p = bridge.spectrum_batch(s, n, hop, cfg["detrend"], cfg["window"], 0, cfg["precision"])
+        p = bridge.spectrum_batch(s, n, hop, cfg["detrend"], cfg["window"], 0, cfg["precision"], out=out)
         ts.append(time.perf_counter() - t0)
 finally:
     bridge.shutdown()
 best = min(ts)
 bytes_moved = (s.size + w * (n // 2)) * 8
 print(json.dumps({"config": cfg, "seconds": ts, "windows_per_s": w / best,
-                  "host_bytes_per_s": bytes_moved / best, "note": "gpu_spectrum_batch from host memory, 1 GPU"}))
+                  "host_bytes_per_s": bytes_moved / best, "registered": registered,
+                  "register_seconds": t_reg if registered else None,
+                  "note": "gpu_spectrum_batch from host memory, 1 GPU" + (
+                      " (series and output registered: DMA in place)" if registered else " (staged)")}))

@@ -110,6 +110,8 @@ hipError_t hipFree(void *p) {
 }
 hipError_t hipHostMalloc(void **p, size_t n, unsigned int) { return hipMalloc(p, n); }
 hipError_t hipHostFree(void *p) { return hipFree(p); }
+hipError_t hipHostRegister(void *, size_t, unsigned int) { return hipSuccess; }
+hipError_t hipHostUnregister(void *) { return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int) {
     *d = h;
     return hipSuccess;

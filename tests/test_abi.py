@@ -120,6 +120,8 @@ def test_no_gpu_fails_loudly_without_fallback():
     st = bridge.lib().gpu_fft_real_forward(bridge._dptr(x), 1024, bridge._dptr(x))
     assert st == bridge.BACKEND_UNAVAILABLE
     assert bridge.lib().wsp_plan_create(0, 1024, 1024, 4, 0, 1, 0, 0, 0) == 0
+    assert bridge.lib().gpu_register_host(bridge._dptr(x), x.size) == bridge.BACKEND_UNAVAILABLE
+    assert bridge.lib().gpu_unregister_host(bridge._dptr(x)) == bridge.BACKEND_UNAVAILABLE
 
 
 def test_harness_binary_built():
