@@ -533,7 +533,13 @@ __device__ __forceinline__ bool kagree(float a, float b, float floor_) {
 //  * the filter reads two steps of both segments per ds_read_b128.
 // With 68-dword rows every one of these LDS accesses is conflict-free: 16 lanes of a b128 access
 // cover the 64 banks once (rows 4 banks apart, 8 lanes of a row 8 banks apart).
-template <int J, int WAVES, int WU = kPk2Warm>
+// ROT (default): the tile loop rotated so that the wait for tile c + 1's loads comes after tile c's
+// stores on every path, and the main pass's stores unconditional (segment B's warm-up values land in
+// segment A's region [L0 - WU, L0), which segment A overwrites later from the same wave): the loads
+// then need vmcnt(#stores) instead of vmcnt(0) (gfx950 counts loads and stores in one in-order
+// counter, and the unrotated loop's entry path and conditional stores forced a wait for the previous
+// tile's stores every J steps).
+template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true>
 __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
                                                                 int64_t hop, int64_t n_windows, int n, KP kp,
                                                                 unsigned *fallbacks = nullptr) {
@@ -577,17 +583,30 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     KState2 st;
     float x0 = 0.f;
     KState<float> warm;  // segment B's state after its warm-up
-    auto run = [&](int c0, int c1, int sA, int sB) {
-        issue(c0);
-        for (int c = c0; c < c1; ++c) {
+    auto stage = [&]() {  // the loaded rows of both segments -> (A, B) pairs in the tile
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                f4v *t = reinterpret_cast<f4v *>(tile + tpos(g));
-                t[0] = f4v{ra[g].x, rb[g].x, ra[g].y, rb[g].y};
-                t[1] = f4v{ra[g].z, rb[g].z, ra[g].w, rb[g].w};
-            }
+        for (int g = 0; g < 8; ++g) {
+            f4v *t = reinterpret_cast<f4v *>(tile + tpos(g));
+            t[0] = f4v{ra[g].x, rb[g].x, ra[g].y, rb[g].y};
+            t[1] = f4v{ra[g].z, rb[g].z, ra[g].w, rb[g].w};
+        }
+    };
+    // store_a: segment A's rows are stored (main pass); segment B's always are (ROT: also during its
+    // warm-up, into segment A's later region)
+    auto run = [&](int c0, int c1, int sA, int sB, auto store_a) {
+        constexpr bool SA = decltype(store_a)::value;
+        issue(c0);
+        if constexpr (ROT) {
+            stage();
             __syncthreads();
-            if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
+            if (c0 + 1 < c1) issue(c0 + 1);
+        }
+        for (int c = c0; c < c1; ++c) {
+            if constexpr (!ROT) {
+                stage();
+                __syncthreads();
+                if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
+            }
             if (c == 0) {
                 const kf2 f = tile[l * RS];  // (sample 0, sample L0 - WU)
                 x0 = f.x;
@@ -626,13 +645,20 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
             for (int g = 0; g < 8; ++g) {
                 const f4v *t = reinterpret_cast<const f4v *>(tile + tpos(g));
                 const f4v u = t[0], v = t[1];
-                if (c >= sA) st4(f4v{u.x, u.z, v.x, v.z}, vc, out_off(g, 0));
-                if (c >= sB) st4(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1));
+                if (ROT ? SA : c >= sA) st4(f4v{u.x, u.z, v.x, v.z}, vc, out_off(g, 0));
+                if (ROT || c >= sB) st4(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1));
             }
             __syncthreads();
+            if constexpr (ROT) {
+                if (c + 1 < c1) {
+                    stage();  // waits for tile c + 1's loads only: this tile's stores stay in flight
+                    __syncthreads();
+                    if (c + 2 < c1) issue(c + 2);
+                }
+            }
         }
     };
-    run(0, nchunks, 0, WUC);
+    run(0, nchunks, 0, WUC, std::true_type{});
     // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it
     const float fl = 0x1p-24f * (fabsf(x0) + fabsf(st.pos.x));
     const bool ok = kagree(st.pos.x, warm.pos, fl) && kagree(st.vel.x, warm.vel, fl) && kagree(st.acc.x, warm.acc, fl) &&
@@ -646,7 +672,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         st.p00.y = st.p00.x, st.p01.y = st.p01.x, st.p02.y = st.p02.x, st.p03.y = st.p03.x;
         st.p11.y = st.p11.x, st.p12.y = st.p12.x, st.p13.y = st.p13.x, st.p22.y = st.p22.x;
         st.p23.y = st.p23.x, st.p33.y = st.p33.x;
-        run(WUC, nchunks, nchunks, WUC);  // only segment B stores
+        run(WUC, nchunks, nchunks, WUC, std::false_type{});  // only segment B stores
     }
 }
 

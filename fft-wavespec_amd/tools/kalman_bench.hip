@@ -52,11 +52,11 @@ __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ i
 }
 
 // the packed two-segment kernel (fp32, default flags)
-template <int WAVES, int WU>
+template <int WAVES, int WU, bool ROT = true>
 void launch_pk2(const float *x, float *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
     const size_t stat = (size_t)WAVES * 64 * 34 * 8;
     const size_t reserve = WAVES == 4 ? 84 * 1024 - stat : 0;
-    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, WAVES, WU>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)), dim3(64 * WAVES),
+    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, WAVES, WU, ROT>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)), dim3(64 * WAVES),
                        reserve, s, x, d, hop, W, n, kp, g_fallbacks);
 }
 
@@ -95,7 +95,7 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     fflush(stdout);
 }
 
-template <int WAVES, int WU, int SEGS = 2>
+template <int WAVES, int WU, int SEGS = 2, bool ROT = true>
 void time_pk2(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n, int reps,
               hipStream_t s) {
     kcore::KP kp;
@@ -107,7 +107,7 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     CK(hipMemset(g_fallbacks, 0, 4));
     auto go = [&]() {
         if constexpr (SEGS == 4) launch_pk4<WU>(x, d, n, W, n, kp, s);
-        else launch_pk2<WAVES, WU>(x, d, n, W, n, kp, s);
+        else launch_pk2<WAVES, WU, ROT>(x, d, n, W, n, kp, s);
     };
     go();
     CK(hipEventRecord(a, s));
@@ -207,6 +207,7 @@ int time_main(int reps) {
         time_pk2<4, 128>("packed 2 segments WU=128, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<4, 256>("packed 2 segments WU=256, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<4, 512>("packed 2 segments WU=512, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<1, 256, 2, false>("packed 2 segments WU=256, 1-wave WG, unrotated", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256>("packed 2 segments WU=256, 1-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256, 4>("packed 4 segments WU=256, lane pairs", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 512, 4>("packed 4 segments WU=512, lane pairs", x, d, ci, co, cn, W, n, reps, s);
@@ -403,7 +404,8 @@ int check_main(int n) {
             CK(hipMemcpy(dx32, xsf.data(), xsf.size() * 4, hipMemcpyHostToDevice));
             CK(hipMemset(g_fallbacks, 0, 4));
             if (segs == 4) launch_pk4<kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
-            else launch_pk2<4, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+            else if (segs == 3) launch_pk2<4, kcore::kPk2Warm, false>(dx32, dd32, hop, W, n, kp, 0);
+            else launch_pk2<1, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
             launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
             CK(hipDeviceSynchronize());
             std::vector<float> h(W * n), q(W * n);
@@ -426,6 +428,8 @@ int check_main(int n) {
         const int L0 = (n + kcore::kPk2Warm) / 2, WU = kcore::kPk2Warm;
         check_pk("f32 packed 2 segments", 2, {});
         check_pk("f32 packed 2 segments, spikes", 2, {L0 - WU});
+        check_pk("f32 packed 2 segments unrotated", 3, {});
+        check_pk("f32 packed 2 segments unrotated, spikes", 3, {L0 - WU});
         if (kcore::pk4_fits(n)) {
             const int S = (n + 3 * WU) / 4 - WU;
             check_pk("f32 packed 4 segments", 4, {});
