@@ -903,30 +903,12 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             // odd samples i0 + 1 + D r: h_(r+1) = 2C h_r - h_(r-1) + a0 (2 - 2C), C = cos(th D) = a.cs.
             // Seeds h_0, h_1 of both sequences from the per-thread rotation start; the recurrence
             // amplifies rounding by at most 1/sin(th D) (~2.6 at R0 = 16) over <= 15 steps.
-            // fp32 plans run the recurrence and the multiply in fp32 from fp64 seeds (the detrend above
-            // stays fp64): 15 steps of rounding amplified <= 2.6x are ~2e-6 of a window value, below
-            // what fp32 samples carry, and the fp64 form's conversions and fp64 issue cost go
-            // (C3's spectrum pass; f32 parity unchanged at the 1e-5 bar).
             const double C2 = 2.0 * a.cs, K = a.a0 * (2.0 - C2);
 #pragma unroll
             for (int q = 0; q < BPT0; ++q) {
                 double c = wc0[q], s = ws0[q];
                 asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no hoisted seeds
                 const double c1 = c * a.cs - s * a.ss, s1 = s * a.cs + c * a.ss;
-                if constexpr (sizeof(T) == 4) {
-                    const float C2f = (float)C2, Kf = (float)K;
-                    float he0 = (float)(a.a0 + a.a1 * c), he1 = (float)(a.a0 + a.a1 * c1);
-                    float ho0 = (float)(a.a0 + a.a1 * (c * a.co - s * a.so)), ho1 = (float)(a.a0 + a.a1 * (c1 * a.co - s1 * a.so));
-#pragma unroll
-                    for (int r = 0; r < R0; ++r) {
-                        v[q * R0 + r] = {(float)xa[q * R0 + r] * he0, (float)xb[q * R0 + r] * ho0};
-                        const float he2 = fmaf(C2f, he1, Kf - he0), ho2 = fmaf(C2f, ho1, Kf - ho0);
-                        he0 = he1;
-                        he1 = he2;
-                        ho0 = ho1;
-                        ho1 = ho2;
-                    }
-                } else {
                 double he0 = a.a0 + a.a1 * c, he1 = a.a0 + a.a1 * c1;
                 double ho0 = a.a0 + a.a1 * (c * a.co - s * a.so), ho1 = a.a0 + a.a1 * (c1 * a.co - s1 * a.so);
 #pragma unroll
@@ -937,7 +919,6 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                     he1 = he2;
                     ho0 = ho1;
                     ho1 = ho2;
-                }
                 }
             }
         } else {
