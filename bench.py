@@ -349,14 +349,30 @@ class C5Batch(Workload):
         nwins = [bars - lens[s // 7] + 1 for s in range(28)]
         sp = shard_plan("c5", rank, world, scaling)
         owned, seed_off = sp["symbols"], sp["seed_offset"]
-        self.streams = [torch.cuda.Stream(dev) for _ in lens]
-        self.jobs = []  # (plan, series, out, stream)
-        for sym in owned:
+        # Three streams, within the box's 4 HIP hardware queues together with the launch stream (with
+        # one stream per length two of them shared a hardware queue and ran 14 kernels back to back:
+        # the whole step, profiles/r02/c5_kernel_stats.csv); symbols assigned to the
+        # least-loaded stream by windows x N log N (C5_LAYOUT=greedy) or by window length (default:
+        # {4096}, {2048}, {1024, 512}).  C5_STREAMS=1 puts every symbol on one stream (ablation).
+        nstreams = int(os.environ.get("C5_STREAMS", "3"))
+        self.streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+        cost = {sym: nwins[sym] * lens[sym // 7] * int(np.log2(lens[sym // 7])) for sym in owned}
+        load, assign = [0] * nstreams, {}
+        if os.environ.get("C5_LAYOUT", "length") == "greedy":
+            for sym in sorted(owned, key=lambda x: -cost[x]):
+                k = load.index(min(load))
+                assign[sym] = k
+                load[k] += cost[sym]
+        else:  # by window length: {4096}, {2048}, {1024, 512}
+            for sym in owned:
+                assign[sym] = {4096: 0, 2048: 1, 1024: 2, 512: 2}[lens[sym // 7]] % nstreams
+        self.jobs = []  # (plan, series, out, stream), launched longest first
+        for sym in sorted(owned, key=lambda x: -cost[x]):
             n = lens[sym // 7]
             series = synth.random_walk_torch(bars, 100 + sym + seed_off, dev)
             out = torch.empty(nwins[sym] * (n // 2), dtype=torch.float64, device=dev)
             self.jobs.append((bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann"), series, out,
-                              self.streams[sym // 7]))
+                              self.streams[assign[sym]]))
         self.stream = torch.cuda.current_stream(dev)
         self.windows = sum(j[0].n_windows for j in self.jobs)
         self.alg_bytes = sum(j[0].algorithmic_bytes for j in self.jobs)
