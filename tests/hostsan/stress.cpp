@@ -9,11 +9,15 @@
 //   * a poller racing gpu_free_job on the same job;
 //   * device plans executed while another thread re-targets (set_topk) and
 //     destroys them;
-//   * gpu_init on another device while the session is open (must be refused).
+//   * gpu_init on another device while the session is open (must be refused);
+//   * pinned feeds (gpu_register_host): threads registering their series and
+//     output arrays, running synchronous batches through them, unregistering,
+//     and two threads racing to register overlapping ranges of one buffer.
 // Every record is checked against the fake kernels' formula
 // (record element k of window w = x[w*hop + k % N] + k).  Exit 0 = all good.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -38,6 +42,8 @@ struct Api {
     decltype(&wsp_plan_execute) plan_execute;
     decltype(&wsp_plan_set_topk) plan_set_topk;
     decltype(&wsp_plan_destroy) plan_destroy;
+    decltype(&gpu_register_host) reg;
+    decltype(&gpu_unregister_host) unreg;
 } A;
 std::atomic<int> g_fail{0};
 
@@ -150,6 +156,41 @@ void plan_race() {  // execute vs set_topk vs destroy on shared plans
         CHECK(A.plan_destroy(p) == MTB_BAD_ARGS, "double destroy");
     }
 }
+void pinned_feed(int sym) {  // FeedCache rewired to pinned buffers, one chart's view
+    CHECK(A.init(0, 16) == MTB_OK, "init pinned %d", sym);
+    const int n = 128 << (sym % 3), hop = 1 + sym % 4, len = 64 * hop + n;
+    const std::vector<double> s = series_of(40 + sym, len);
+    const int nwin = 1 + (len - n) / hop, rec = n / 2;
+    std::vector<double> out((size_t)nwin * rec);
+    for (int r = 0; r < 20; ++r) {
+        CHECK(A.reg(s.data(), len) == MTB_OK, "register series %d", sym);
+        CHECK(A.reg(s.data() + 1, 8) == MTB_BAD_ARGS, "overlap refused %d", sym);
+        CHECK(A.reg(out.data(), (int64_t)out.size()) == MTB_OK, "register out %d", sym);
+        std::fill(out.begin(), out.end(), -1.0);
+        int got = 0;
+        CHECK(A.batch(s.data(), len, n, hop, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, out.data(),
+                      (int)out.size(), &got) == MTB_OK && got == nwin, "pinned batch %d", sym);
+        CHECK(check_records(s, out.data(), n, hop, nwin, rec), "pinned records %d round %d", sym, r);
+        CHECK(A.unreg(out.data()) == MTB_OK && A.unreg(s.data()) == MTB_OK, "unregister %d", sym);
+        CHECK(A.unreg(s.data()) == MTB_BAD_ARGS, "double unregister %d", sym);
+    }
+    A.shutdown();
+}
+
+void register_race() {  // two threads register overlapping ranges of one buffer: exactly one wins
+    CHECK(A.init(0, 16) == MTB_OK, "init race");
+    std::vector<double> buf(1 << 16);
+    for (int r = 0; r < 50; ++r) {
+        std::atomic<int> ok{0};
+        std::thread a([&] { ok += A.reg(buf.data(), 1 << 15) == MTB_OK; });
+        std::thread b([&] { ok += A.reg(buf.data() + 1000, 1 << 14) == MTB_OK; });
+        a.join();
+        b.join();
+        CHECK(ok == 1, "overlapping registrations: %d succeeded", ok.load());
+        CHECK(A.unreg(buf.data()) == MTB_OK || A.unreg(buf.data() + 1000) == MTB_OK, "unregister the winner");
+    }
+    A.shutdown();
+}
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -170,6 +211,8 @@ int main(int argc, char **argv) {
     sym(h, A.plan_execute, "wsp_plan_execute");
     sym(h, A.plan_set_topk, "wsp_plan_set_topk");
     sym(h, A.plan_destroy, "wsp_plan_destroy");
+    sym(h, A.reg, "gpu_register_host");
+    sym(h, A.unreg, "gpu_unregister_host");
 
     // the session outlives every chart below; a different device is refused while it is open
     CHECK(A.init(0, 8) == MTB_OK, "main init");
@@ -179,6 +222,8 @@ int main(int argc, char **argv) {
     for (int c = 0; c < 28; ++c) th.emplace_back(chart, c, c % 2 == 0, std::ref(early_done), 6);
     th.emplace_back(free_race);
     th.emplace_back(plan_race);
+    for (int c = 0; c < 4; ++c) th.emplace_back(pinned_feed, c);
+    th.emplace_back(register_race);
     for (auto &t : th) t.join();
     CHECK(early_done == 14, "early charts %d", early_done.load());
     // main's own reference still holds the session: a sync batch works

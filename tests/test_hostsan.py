@@ -4,7 +4,8 @@ tests/hostsan builds csrc/mtbridge.cpp against fake_hip.cpp -- a test double of 
 real asynchronous streams (worker threads) and launch stubs that write a checkable function of each
 window -- under -fsanitize=thread and -fsanitize=address,undefined, and drives the C ABI from 30
 threads (stress.cpp): 28 charts with staggered gpu_shutdown, a poller racing gpu_free_job, plans
-executed while being re-targeted and destroyed.  The round-1 library fails this driver (12 TSAN
+executed while being re-targeted and destroyed, pinned feeds registered / used / unregistered from
+several threads and two threads racing to register overlapping ranges.  The round-1 library fails this driver (12 TSAN
 reports, profiles/r02/hostsan_stress.txt); the current one must pass it clean.
 """
 import shutil
