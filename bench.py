@@ -61,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--config", default="north_star", choices=CONFIGS)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
+    ap.add_argument("--algo", default="auto", choices=["auto", "fft", "slide"],
+                    help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
@@ -280,7 +282,7 @@ def shard_plan(name: str, rank: int, world: int, scaling: str) -> dict:
 class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
-    def __init__(self, name, rank, local_rank, world, scaling):
+    def __init__(self, name, rank, local_rank, world, scaling, algo="auto"):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -308,6 +310,9 @@ class SingleBatch(Workload):
                                     cfg["precision"], output)
             if output in ("topk", "topk_phase"):
                 self.plan.set_topk(8, 18.0, 200.0)  # the reference's scan (1.1.0:22-23)
+            if algo != "auto":
+                self.plan.set_algorithm(algo)
+        self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
         del full
         self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
         self.stream = torch.cuda.current_stream(dev)
@@ -318,7 +323,7 @@ class SingleBatch(Workload):
         self.f32 = f32
         self.cfg = cfg
         self.cpu_cfg = (self.series, cfg)
-        self.traffic = load_traffic(name)
+        self.traffic = load_traffic(name if algo == "auto" else f"{name}_{algo}")
         shard = f", windows [{w0}, {w0 + nw}) of {w}" if scaling == "strong" else ""
         self.describe = (f"{name}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, {cfg['detrend']} detrend, "
                          f"{cfg['window']} window, " + {
@@ -341,7 +346,7 @@ class C5Batch(Workload):
     symbol).  One step = every owned symbol's batch; each window length runs on its own stream,
     joined into the launch stream."""
 
-    def __init__(self, rank, local_rank, world, scaling):
+    def __init__(self, rank, local_rank, world, scaling, algo="auto"):
         import torch
         from wavespec_amd import bridge, synth
         dev = torch.device("cuda", local_rank)
@@ -371,12 +376,15 @@ class C5Batch(Workload):
             n = lens[sym // 7]
             series = synth.random_walk_torch(bars, 100 + sym + seed_off, dev)
             out = torch.empty(nwins[sym] * (n // 2), dtype=torch.float64, device=dev)
-            self.jobs.append((bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann"), series, out,
-                              self.streams[assign[sym]]))
+            plan = bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann")
+            if algo != "auto":
+                plan.set_algorithm(algo)
+            self.jobs.append((plan, series, out, self.streams[assign[sym]]))
+        self.algorithm = "+".join(sorted({j[0].algorithm() for j in self.jobs}))
         self.stream = torch.cuda.current_stream(dev)
         self.windows = sum(j[0].n_windows for j in self.jobs)
         self.alg_bytes = sum(j[0].algorithmic_bytes for j in self.jobs)
-        per_launch = load_traffic("c5")  # PMC bytes per spectrum dispatch; one step is len(jobs) dispatches
+        per_launch = load_traffic("c5" if algo == "auto" else f"c5_{algo}")  # PMC bytes per spectrum dispatch; one step is len(jobs) dispatches
         self.traffic = per_launch * len(self.jobs) if per_launch else None
         self.f32 = False
         big = [j for j in self.jobs if j[0].window_len == 4096]
@@ -425,9 +433,9 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     ctl = Control(world)
     if args.config == "c5":
-        wl = C5Batch(rank, local_rank, world, args.scaling)
+        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo)
     else:
-        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling)
+        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)
@@ -459,7 +467,8 @@ def main(argv=None):
             "dtype": "f32" if wl.f32 else "f64",
             "data": "synthetic (random-walk close prices generated on device, seed per rank)",
             "config": {"workload": wl.describe, "windows_per_gpu": wl.windows, "windows_total": int(total_windows / args.steps),
-                       "parallelism": f"windows sharded x{world} ({args.scaling}), no collective"},
+                       "parallelism": f"windows sharded x{world} ({args.scaling}), no collective",
+                       "algorithm": wl.algorithm},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
                          "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,

@@ -210,6 +210,85 @@ int get_tables(int dev, int log2n, bool f32, Tables *out) {
     return MTB_OK;
 }
 
+// Sliding-DFT tables per (device, N, window) (sliding_dft.hip), double complex, long double
+// arithmetic rounded once: [nf][N/2] omega_f(k) = e^{2 pi j (k/N + m_f/(N-1))}, m_f = 0, +1, -1, +2, -2;
+// [N/2] H_k = DFT_k of the window; [(nf-1)/2][N] e^{-j m th i}, th = 2 pi/(N-1).
+struct WinCoef {
+    double a0 = 1.0, a1 = 0.0, a2 = 0.0;
+    int nf = 1;  // complex exponentials in the window (0 = not a cosine sum: Bartlett)
+};
+// L/WaveSpecZZ_1.0.2.mq5:884-922 as a0 + a1 cos(th i) + a2 cos(2 th i)
+WinCoef window_coef(int window) {
+    WinCoef w;
+    switch (window) {
+    case MTB_WINDOW_HANN: w.a0 = 0.5, w.a1 = -0.5, w.nf = 3; break;
+    case MTB_WINDOW_HAMMING: w.a0 = 0.54, w.a1 = -0.46, w.nf = 3; break;
+    case MTB_WINDOW_BLACKMAN: w.a0 = 0.42, w.a1 = -0.5, w.a2 = 0.08, w.nf = 5; break;
+    case MTB_WINDOW_BARTLETT: w.nf = 0; break;
+    default: break;
+    }
+    return w;
+}
+std::mutex g_slide_mu;
+std::map<std::tuple<int, int, int>, void *> *g_slide_tables = new std::map<std::tuple<int, int, int>, void *>();
+
+int get_slide_table(int dev, int log2n, int window, void **out) {
+    std::lock_guard<std::mutex> lk(g_slide_mu);
+    auto key = std::make_tuple(dev, log2n, window);
+    auto it = g_slide_tables->find(key);
+    if (it != g_slide_tables->end()) {
+        *out = it->second;
+        return MTB_OK;
+    }
+    typedef long double ld;
+    const ld pi = 3.141592653589793238462643383279502884L;
+    const WinCoef wc = window_coef(window);
+    const int n = 1 << log2n, m2 = n / 2, nf = wc.nf, nm = (nf - 1) / 2;
+    const int mf[5] = {0, 1, -1, 2, -2};
+    const ld sc[5] = {(ld)wc.a0, (ld)wc.a1 / 2, (ld)wc.a1 / 2, (ld)wc.a2 / 2, (ld)wc.a2 / 2};
+    std::vector<double> tab((size_t)2 * ((size_t)(nf + 1) * m2 + (size_t)nm * n));
+    double *om = tab.data(), *hw = om + (size_t)2 * nf * m2, *md = hw + (size_t)2 * m2;
+    for (int f = 0; f < nf; ++f)
+        for (int k = 0; k < m2; ++k) {
+            const ld ang = 2 * pi * ((ld)k / n + (ld)mf[f] / (n - 1));
+            om[2 * ((size_t)f * m2 + k)] = (double)cosl(ang);
+            om[2 * ((size_t)f * m2 + k) + 1] = (double)sinl(ang);
+        }
+    // H_k = sum_f s_f G(k/N + m_f/(N-1)), G(g) = sum_{i<N} e^{-2 pi j g i}
+    //     = e^{-j pi g (N-1)} sin(pi g N)/sin(pi g), with sin(pi g N) = (-1)^(k+m) sin(pi m/(N-1))
+    for (int k = 0; k < m2; ++k) {
+        ld hr = 0, hi = 0;
+        for (int f = 0; f < nf; ++f) {
+            if (sc[f] == 0) continue;
+            const ld g = (ld)k / n + (ld)mf[f] / (n - 1);
+            ld gr, gi;
+            if (k == 0 && mf[f] == 0) {
+                gr = n, gi = 0;
+            } else {
+                const ld num = (((k + mf[f]) & 1) ? -1 : 1) * sinl(pi * (ld)mf[f] / (n - 1));
+                const ld mag = num / sinl(pi * g);
+                const ld ph = -pi * ((ld)k * (n - 1) / n + (ld)mf[f]);
+                gr = mag * cosl(ph), gi = mag * sinl(ph);
+            }
+            hr += sc[f] * gr, hi += sc[f] * gi;
+        }
+        hw[2 * k] = (double)hr, hw[2 * k + 1] = (double)hi;
+    }
+    for (int m = 1; m <= nm; ++m)
+        for (int i = 0; i < n; ++i) {
+            const ld ang = -2 * pi * (ld)m * (ld)i / (n - 1);
+            md[2 * ((size_t)(m - 1) * n + i)] = (double)cosl(ang);
+            md[2 * ((size_t)(m - 1) * n + i) + 1] = (double)sinl(ang);
+        }
+    void *d = nullptr;
+    HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    HIP_OR(hipMalloc(&d, tab.size() * sizeof(double)), MTB_NO_MEM);
+    HIP_OR(hipMemcpy(d, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
+    (*g_slide_tables)[key] = d;
+    *out = d;
+    return MTB_OK;
+}
+
 // ----------------------------------------------------------------- config
 enum Op : int { kOpSpectrum = 0, kOpInverse = 1 };
 struct Config {
@@ -218,6 +297,7 @@ struct Config {
     int64_t hop = 0, n_windows = 0;
     int detrend = 0, window = 0, trend_period = 0, output = 0;
     int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK / MTB_OUT_TOPK_PHASE
+    int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
     int64_t record() const {
@@ -334,6 +414,19 @@ int config_set_topk(Config *c, int top_k, double min_period, double max_period) 
 std::mutex g_kalman_mu;
 double g_kalman[16] = {1.0, 0.01, 0.003, 0.0008, 0.0002, 0.8, 1.0, 16.0, 9.0, 4.0, 1.0, 0.0, 0.0, 0.0, 6.0, 0.0};
 
+// hop = 1 power batches by the seeded sliding DFT (sliding_dft.hip) instead of an FFT per window:
+// the windows' trackers slide by one sample exactly, ~2.5x less fp64 work per window.
+bool slide_eligible(const Config &c) {
+    const int nf = window_coef(c.window).nf;
+    return c.op == kOpSpectrum && c.hop == 1 && c.output == MTB_OUT_POWER && c.log2n >= kSlideMinLog2N &&
+           c.log2n <= kSlideMaxLog2N && (c.detrend == MTB_DETREND_NONE || c.detrend == MTB_DETREND_MEAN) &&
+           nf > 0 && !(nf == 5 && c.log2n == kSlideMaxLog2N);  // Blackman at N = 8192 spills at 1024 threads
+}
+bool use_slide(const Config &c) {
+    if (c.algo == MTB_ALGO_FFT || !slide_eligible(c)) return false;
+    return c.algo == MTB_ALGO_SLIDE || c.n_windows >= 256;
+}
+
 // ------------------------------------------------------------ device path
 // series (device) -> [Kalman pre-pass into ws] -> spectrum kernel -> out.
 int enqueue(int dev, const Config &c, const double *kalman, const void *d_series, void *d_out, void *d_ws,
@@ -389,6 +482,31 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         G.packed = c.output == MTB_OUT_PACKED;
         G.f32 = c.f32;
         HIP_OR(launch_large(G, s), MTB_INTERNAL_ERROR);
+        return MTB_OK;
+    }
+    if (use_slide(c)) {
+        Tables t64;
+        void *stab = nullptr;
+        if ((st = get_tables(dev, c.log2n, false, &t64)) != MTB_OK) return st;
+        if ((st = get_slide_table(dev, c.log2n, c.window, &stab)) != MTB_OK) return st;
+        HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+        const WinCoef wc = window_coef(c.window);
+        const long double th = 2.0L * 3.141592653589793238462643383279502884L / (long double)(c.n - 1);
+        SlideArgs A{};
+        A.series = d_series;
+        A.out = d_out;
+        A.twiddle = t64.tw;
+        A.omega = stab;
+        A.n_windows = c.n_windows;
+        A.seg = slide_segment(c.n_windows);
+        A.log2n = c.log2n;
+        A.nf = wc.nf;
+        A.detrend = c.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
+        A.f32 = c.f32;
+        A.s0 = wc.a0, A.s1 = wc.a1 / 2, A.s2 = wc.a2 / 2;
+        A.c1 = (double)cosl(th), A.sn1 = (double)sinl(th), A.c2 = (double)cosl(2 * th), A.sn2 = (double)sinl(2 * th);
+        A.inv_n = 1.0 / c.n;
+        HIP_OR(launch_slide(A, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
     SpectrumLaunch L{};
@@ -1384,6 +1502,35 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
     const int st = config_set_topk(&c, top_k, min_period, max_period);
     if (st == MTB_OK) p->cfg = c;
     return st;
+}
+
+MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p) {
+        set_error("unknown plan %lld", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (algo < MTB_ALGO_AUTO || algo > MTB_ALGO_SLIDE) {
+        set_error("algorithm %d: MTB_ALGO_AUTO, MTB_ALGO_FFT or MTB_ALGO_SLIDE", algo);
+        return MTB_BAD_ARGS;
+    }
+    Config c = p->cfg;
+    c.algo = algo;
+    if (algo == MTB_ALGO_SLIDE && !slide_eligible(c)) {
+        set_error("plan %lld: the sliding DFT takes hop = 1, N = 512..8192, detrend none/mean, a cosine window "
+                  "and power output", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    p->cfg = c;
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_plan_get_algorithm(int64_t plan) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p) return MTB_BAD_ARGS;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return use_slide(p->cfg) ? MTB_ALGO_SLIDE : MTB_ALGO_FFT;
 }
 
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan) {

@@ -1,0 +1,241 @@
+// sliding_dft.hip -- hop = 1 batches by a seeded sliding DFT (gfx950).
+//
+// The same quantity as spectrum_kernel -- per window w: x[w .. w+N) -> [mean detrend] -> cosine
+// window (L/WaveSpecZZ_1.0.2.mq5:884-922) -> DFT (FourierTransformManual, :938-974) -> |X_k|^2,
+// k < N/2 (1.1.0:529-530) -- for consecutive windows (hop = 1 bar, the batch-warmup and
+// fetcher shape: 1.1.0:1014-1020, WaveCyclesBatchFetcher.mq5:106-133), computed by a different
+// exact-in-real-arithmetic route that does ~2.5x less fp64 work per window than an FFT.
+//
+// With the window a0 + a1 cos(th i) + a2 cos(2 th i), th = 2 pi/(N-1), and
+// S_w(f) = sum_i x[w+i] e^{-2 pi j f i}:
+//     X_w[k] = a0 S_w(k/N) + a1/2 (S_w(k/N + phi) + S_w(k/N - phi)) + a2/2 (S_w(k/N +- 2 phi)),
+//     phi = 1/(N-1).
+// Each S slides by one sample exactly:
+//     S_{w+1}(f) = e^{2 pi j f} (S_w(f) - x[w] + x[w+N] e^{-2 pi j f N}),
+// and for f = k/N + m phi the factor e^{-2 pi j f N} = e^{-j m th} is the same for every bin, so
+// one step of one tracker T_f = s_f S_f is T <- omega_f (T + u_m) with a per-step uniform u_m:
+// 5-6 fp64 operations per tracker, 23 per bin and window for Hann (|X|^2 included) against
+// ~57 for the radix-16/8 FFT at N = 2048.  The mean detrend is linear:
+// X_w - mean_w * H[k], H = DFT of the window.
+//
+// Layout: one workgroup per segment of R consecutive windows, N/(2B) threads, thread t owns
+// bins k = t + NT b (b < B), so every store instruction of a wave writes 64 consecutive bins
+// (512 B).  The segment's trackers are SEEDED exactly, not slid from the previous segment:
+// Y_m = FFT_N(x[w0 + i] e^{-j m th i}) in LDS (radix-2 Stockham, table twiddles) gives
+// S(k/N + m phi) = Y_m[k] and S(k/N - m phi) = conj(Y_m[N-k]).  The per-step uniforms
+// (u_0, u_1, u_2, x[w+N] - x[w]) of the whole segment are staged in LDS, read by broadcast.
+// With the mean detrend the trackers follow the samples minus the segment's first sample.
+// Rounding: a tracker's error grows at most linearly over R <= 512 steps (~5e-14 of its own
+// magnitude); the parity bars are BASELINE.md 2's (tests/test_gpu_parity.py, test_gpu_fullgrid.py).
+#include "wsp_internal.h"
+
+namespace wsp {
+namespace {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int kSlideB = 4;       // bins per thread
+constexpr int kSlideRMax = 512;  // windows per segment (LDS staging of the per-step uniforms)
+
+template <int NF> struct Rec { static constexpr int n = NF + 1; };  // [u0, (u1r, u1i), (u2r, u2i), d]
+
+__device__ __forceinline__ d2 cmul(d2 a, d2 b) { return d2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+
+// In-place natural-order complex FFT of N points in LDS (Stockham radix 2, DIT), NT threads,
+// twiddles W_N^k from the table (k < N/2).  Ends after a barrier.
+template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, const d2 *__restrict__ tw) {
+    constexpr int N = 1 << LOG2N, H = N / 2, Q = H / NT;
+    const int t = threadIdx.x;
+    for (int s = 0; s < LOG2N; ++s) {
+        const int ns = 1 << s;
+        d2 a[Q], b[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            a[q] = buf[t + NT * q];
+            b[q] = buf[t + NT * q + H];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = t + NT * q, k = j & (ns - 1);
+            const d2 bw = cmul(b[q], tw[k << (LOG2N - 1 - s)]);
+            const int d = ((j - k) << 1) + k;
+            buf[d] = a[q] + bw;
+            buf[d + ns] = a[q] - bw;
+        }
+        __syncthreads();
+    }
+}
+
+template <typename T, int LOG2N, int NF, int DETREND>
+__global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 3 ? 3 : 4)) void slide_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, B = kSlideB, NT = M / B;
+    constexpr int NM = (NF - 1) / 2;  // modulations m = 1..NM
+    constexpr int REC = Rec<NF>::n;
+    constexpr int LDS2 = (N > kSlideRMax * REC / 2) ? N : kSlideRMax * REC / 2;
+    __shared__ d2 lds[LDS2];
+    __shared__ double sum0;
+
+    const int t = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
+    const T *__restrict__ x = static_cast<const T *>(a.series) + w0;
+    const d2 *__restrict__ tw = static_cast<const d2 *>(a.twiddle);
+    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);  // [NF][M]
+    const d2 *__restrict__ hwin = omega + NF * M;                      // [M]
+    const d2 *__restrict__ mod = hwin + M;                             // [NM][N]
+
+    d2 om[B][NF], tr[B][NF];
+    // mean detrend: the trackers follow x - L, L = the segment's first sample, and the output subtracts
+    // (mean - L) H_k: X_w - mean_w H = X(x - L) - (mean_w - L) H.  Centring keeps the ~N x price level
+    // out of the trackers near DC (20x smaller rounding at bins 0-2, tests/test_slide_model.py).
+    const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
+
+    // ---- seeds: trackers of window w0 from NM + 1 complex FFTs
+#pragma unroll
+    for (int m = 0; m <= NM; ++m) {
+        for (int i = t; i < N; i += NT) {
+            const double xi = (double)x[i] - lvl;
+            lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
+        }
+        __syncthreads();
+        fft_lds<LOG2N, NT>(lds, tw);
+        const double s = m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int k = t + NT * b;
+            if (m == 0) {
+                tr[b][0] = s * lds[k];
+            } else {
+                const d2 yp = lds[k], ym = lds[(N - k) & (N - 1)];
+                tr[b][2 * m - 1] = s * yp;
+                tr[b][2 * m] = s * d2{ym.x, -ym.y};
+            }
+        }
+        if (DETREND == kDetrendMean && m == 0 && t == 0) sum0 = lds[0].x;
+        __syncthreads();
+    }
+
+    // ---- per-step uniforms of the segment: u_m = s_m (x[w+N] e^{-j m th} - x[w]), d = x[w+N] - x[w]
+    double *u = reinterpret_cast<double *>(lds);
+    for (int st = t; st < len - 1; st += NT) {
+        const double xw = (double)x[st] - lvl, xn = (double)x[st + N] - lvl;
+        double *r = u + st * REC;
+        r[0] = a.s0 * (xn - xw);
+        if constexpr (NF >= 3) {
+            r[1] = a.s1 * (xn * a.c1 - xw);
+            r[2] = -(a.s1 * (xn * a.sn1));
+        }
+        if constexpr (NF >= 5) {
+            r[3] = a.s2 * (xn * a.c2 - xw);
+            r[4] = -(a.s2 * (xn * a.sn2));
+        }
+        r[REC - 1] = xn - xw;
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) om[b][f] = omega[f * M + t + NT * b];
+    d2 hk[B];
+    double sum = 0.0;
+    if constexpr (DETREND == kDetrendMean) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) hk[b] = hwin[t + NT * b];
+        sum = sum0;
+    }
+
+    // ---- slide
+    T *__restrict__ out = static_cast<T *>(a.out) + w0 * M + t;
+#pragma unroll 1
+    for (int st = 0; st < len; ++st) {
+        double mw = 0.0;
+        if constexpr (DETREND == kDetrendMean) mw = sum * a.inv_n;
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            d2 X = tr[b][0];
+#pragma unroll
+            for (int f = 1; f < NF; ++f) X += tr[b][f];
+            if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
+            const double p = X.x * X.x + X.y * X.y;
+            __builtin_nontemporal_store((T)p, out + NT * b);
+        }
+        out += M;
+        if (st + 1 < len) {
+            const double *r = u + st * REC;
+            const double u0 = r[0];
+#pragma unroll
+            for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
+            if constexpr (NF >= 3) {
+                const double u1r = r[1], u1i = r[2];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
+                    tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
+                }
+            }
+            if constexpr (NF >= 5) {
+                const double u2r = r[3], u2i = r[4];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
+                    tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
+                }
+            }
+            if constexpr (DETREND == kDetrendMean) sum += r[REC - 1];
+        }
+    }
+}
+
+template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a, hipStream_t s) {
+    constexpr int NT = (1 << LOG2N) / (2 * kSlideB);
+    const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
+    hipLaunchKernelGGL((slide_kernel<T, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename T, int LOG2N, int NF> hipError_t by_detrend(const SlideArgs &a, hipStream_t s) {
+    return a.detrend == kDetrendMean ? launch_t<T, LOG2N, NF, kDetrendMean>(a, s)
+                                     : launch_t<T, LOG2N, NF, kDetrendNone>(a, s);
+}
+
+template <typename T, int LOG2N> hipError_t by_nf(const SlideArgs &a, hipStream_t s) {
+    switch (a.nf) {
+    case 1: return by_detrend<T, LOG2N, 1>(a, s);
+    case 3: return by_detrend<T, LOG2N, 3>(a, s);
+    case 5: return by_detrend<T, LOG2N, 5>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename T> hipError_t by_n(const SlideArgs &a, hipStream_t s) {
+    switch (a.log2n) {
+    case 9: return by_nf<T, 9>(a, s);
+    case 10: return by_nf<T, 10>(a, s);
+    case 11: return by_nf<T, 11>(a, s);
+    case 12: return by_nf<T, 12>(a, s);
+    case 13: return by_nf<T, 13>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+int64_t slide_segment(int64_t n_windows) {
+    // ~2048 segments (2 workgroups per CU, ~5% seeding cost at R = 512), 64 <= R <= 512
+    int64_t r = (n_windows + 2047) / 2048;
+    if (r < 64) r = 64;
+    if (r > kSlideRMax) r = kSlideRMax;
+    return r;
+}
+
+hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {
+    if (a.n_windows <= 0) return hipSuccess;
+    if (a.seg < 1 || a.seg > kSlideRMax || a.log2n < kSlideMinLog2N || a.log2n > kSlideMaxLog2N)
+        return hipErrorInvalidValue;
+    return a.f32 ? by_n<float>(a, s) : by_n<double>(a, s);
+}
+
+}  // namespace wsp

@@ -98,4 +98,25 @@ struct KalmanLaunch {
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream);
 
+// hop = 1 batches by a seeded sliding DFT (sliding_dft.hip): N = 512 .. 8192, detrend none or
+// mean, windows none / Hann / Hamming / Blackman (sums of nf = 1, 3, 5 complex exponentials),
+// power output.  Arithmetic in fp64 for both element types.
+constexpr int kSlideMinLog2N = 9;
+constexpr int kSlideMaxLog2N = 13;
+struct SlideArgs {
+    const void *series;   // window w at series + w (elements)
+    void *out;            // n_windows rows of N/2 powers
+    const void *twiddle;  // N complex W_N^k (double) -- the seed FFTs
+    const void *omega;    // slide table (double complex): [nf][N/2] e^{2 pi j f}, [N/2] H_k, [(nf-1)/2][N] e^{-j m th i}
+    int64_t n_windows;
+    int64_t seg;          // windows per workgroup (slide_segment)
+    int log2n, nf, detrend;
+    bool f32;
+    double s0, s1, s2;    // a0, a1/2, a2/2
+    double c1, sn1, c2, sn2;  // cos / sin of th and 2 th, th = 2 pi/(N-1)
+    double inv_n;
+};
+hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
+int64_t slide_segment(int64_t n_windows);
+
 }  // namespace wsp

@@ -64,6 +64,8 @@ SIGNATURES = {
     "gpu_spectrum_topk_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                             C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32, _i32p]),
     "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
+    "wsp_plan_set_algorithm": (C.c_int32, [C.c_int64, C.c_int32]),
+    "wsp_plan_get_algorithm": (C.c_int32, [C.c_int64]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -294,6 +296,16 @@ class Plan:
     def set_topk(self, top_k: int, min_period: float, max_period: float) -> None:
         _check("wsp_plan_set_topk", lib().wsp_plan_set_topk(self.handle, top_k, min_period, max_period))
         self.record = (6 if self.output == "topk_phase" else 4) * top_k
+
+    ALGOS = {"auto": 0, "fft": 1, "slide": 2}
+
+    def set_algorithm(self, algo: str) -> None:
+        """wsp_plan_set_algorithm: "auto", "fft" or "slide" (hop = 1 seeded sliding DFT)."""
+        _check("wsp_plan_set_algorithm", lib().wsp_plan_set_algorithm(self.handle, self.ALGOS[algo]))
+
+    def algorithm(self) -> str:
+        """What the next execute runs: "fft" or "slide"."""
+        return {1: "fft", 2: "slide"}[lib().wsp_plan_get_algorithm(self.handle)]
 
     @property
     def algorithmic_bytes(self) -> int:

@@ -255,6 +255,20 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
  * power/packed plan switches to it) or MTB_OUT_TOPK_PHASE (6*top_k). */
 MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period);
 
+/* Algorithm for hop = 1 batches (an extension; the reference always runs an
+ * FFT per window).  MTB_ALGO_AUTO (default): the seeded sliding DFT when the
+ * plan is eligible -- hop = 1, window_len 512..8192, detrend none or mean,
+ * Hann / Hamming / Blackman / no window, MTB_OUT_POWER -- and has at least 256
+ * windows, otherwise the per-window FFT.  MTB_ALGO_FFT / MTB_ALGO_SLIDE force
+ * one (MTB_BAD_ARGS if the plan is not eligible for the slide).  Both produce
+ * the same spectra within the parity bars. */
+#define MTB_ALGO_AUTO 0
+#define MTB_ALGO_FFT 1
+#define MTB_ALGO_SLIDE 2
+MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
+/* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
+MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
+
 /* Bytes the plan's algorithm must move per execute: unique input samples
  * + output, for roofline accounting. */
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan);

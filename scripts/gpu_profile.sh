@@ -3,17 +3,18 @@
 #   1) --kernel-trace --stats      (per-kernel durations)
 #   2) --pmc FETCH_SIZE            (own pass; HBM read bytes, x2 gfx950 correction)
 #   3) --pmc WRITE_SIZE            (own pass)
-# Usage: bash scripts/gpu_profile.sh <tag> [config]
+# Usage: bash scripts/gpu_profile.sh <tag> [config] [algo: auto|fft|slide]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-TAG=$1; CFG=${2:-north_star}
-OUT=gpurun_out/prof_${TAG}_${CFG}
+TAG=$1; CFG=${2:-north_star}; ALGO=${3:-auto}
+KEY=$CFG; [ "$ALGO" = auto ] || KEY=${CFG}_$ALGO
+OUT=gpurun_out/prof_${TAG}_${KEY}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py --config $CFG --steps 100 --warmup 20 --no-cpu-baseline > $OUT/trace.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 100 --warmup 20 --no-cpu-baseline --algo $ALGO > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
-  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
-  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1 || exit $?
-python3 scripts/parse_prof.py $OUT $CFG
+  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO > $OUT/write.log 2>&1 || exit $?
+python3 scripts/parse_prof.py $OUT $CFG $KEY

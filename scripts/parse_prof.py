@@ -4,7 +4,7 @@ Prints per-kernel average duration of our kernels (kernel trace) and the HBM
 bytes per launch from the PMC passes, corrected as MI355X_MICROARCH.md
 sec. HBM prescribes: FETCH_SIZE (KiB) x 1024 x 2 (gfx950 reports half of a
 wide coalesced streaming read), WRITE_SIZE (KiB) x 1024.  Merges the result
-into profiles/traffic.json under the config name.
+into profiles/traffic.json under the config name (or the key given as a third argument).
 """
 import csv
 import glob
@@ -13,9 +13,10 @@ import sys
 from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
-OURS = ("spectrum_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
+key = sys.argv[3] if len(sys.argv) > 3 else cfg  # e.g. c4_fft: the config under a forced algorithm
+OURS = ("spectrum_kernel", "slide_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
         "iir_kernel")
-MAIN = ("spectrum_kernel", "inverse_kernel", "row_kernel")  # one per step; a Kalman pre-pass adds to its step
+MAIN = ("spectrum_kernel", "slide_kernel", "inverse_kernel", "row_kernel")  # one per step; a Kalman pre-pass adds to its step
 
 
 def rows(pattern):
@@ -69,6 +70,6 @@ if fetch is not None and write is not None:
 print(json.dumps(res, indent=1))
 tj = Path("profiles/traffic.json")
 allres = json.loads(tj.read_text()) if tj.exists() else {}
-allres[cfg] = res
+allres[key] = res
 tj.parent.mkdir(exist_ok=True)
 tj.write_text(json.dumps(allres, indent=1))
