@@ -63,6 +63,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the 1-core CPU baseline sample")
     ap.add_argument("--algo", default="auto", choices=["auto", "fft", "slide"],
                     help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
+    ap.add_argument("--slide-seg", type=int, default=0, help="windows per sliding-DFT workgroup (0 = library policy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
@@ -282,7 +283,7 @@ def shard_plan(name: str, rank: int, world: int, scaling: str) -> dict:
 class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
-    def __init__(self, name, rank, local_rank, world, scaling, algo="auto"):
+    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -312,6 +313,8 @@ class SingleBatch(Workload):
                 self.plan.set_topk(8, 18.0, 200.0)  # the reference's scan (1.1.0:22-23)
             if algo != "auto":
                 self.plan.set_algorithm(algo)
+            if slide_seg:
+                self.plan.set_slide_segment(slide_seg)
         self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
         del full
         self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
@@ -346,7 +349,7 @@ class C5Batch(Workload):
     symbol).  One step = every owned symbol's batch; each window length runs on its own stream,
     joined into the launch stream."""
 
-    def __init__(self, rank, local_rank, world, scaling, algo="auto"):
+    def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0):
         import torch
         from wavespec_amd import bridge, synth
         dev = torch.device("cuda", local_rank)
@@ -379,6 +382,8 @@ class C5Batch(Workload):
             plan = bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann")
             if algo != "auto":
                 plan.set_algorithm(algo)
+            if slide_seg:
+                plan.set_slide_segment(slide_seg)
             self.jobs.append((plan, series, out, self.streams[assign[sym]]))
         self.algorithm = "+".join(sorted({j[0].algorithm() for j in self.jobs}))
         self.stream = torch.cuda.current_stream(dev)
@@ -433,9 +438,9 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     ctl = Control(world)
     if args.config == "c5":
-        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo)
+        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
     else:
-        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo)
+        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)

@@ -298,6 +298,7 @@ struct Config {
     int detrend = 0, window = 0, trend_period = 0, output = 0;
     int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK / MTB_OUT_TOPK_PHASE
     int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
+    int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
     int64_t record() const {
@@ -498,7 +499,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         A.twiddle = t64.tw;
         A.omega = stab;
         A.n_windows = c.n_windows;
-        A.seg = slide_segment(c.n_windows);
+        A.seg = c.slide_seg;
         A.log2n = c.log2n;
         A.nf = wc.nf;
         A.detrend = c.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1523,6 +1524,18 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
         return MTB_BAD_ARGS;
     }
     p->cfg = c;
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || windows < 0) {
+        set_error("wsp_plan_set_slide_segment(%lld, %lld): unknown plan or negative length", (long long)plan,
+                  (long long)windows);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.slide_seg = windows;
     return MTB_OK;
 }
 

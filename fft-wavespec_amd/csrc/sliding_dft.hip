@@ -18,15 +18,19 @@
 // ~57 for the radix-16/8 FFT at N = 2048.  The mean detrend is linear:
 // X_w - mean_w * H[k], H = DFT of the window.
 //
-// Layout: one workgroup per segment of R consecutive windows, N/(2B) threads, thread t owns
-// bins k = t + NT b (b < B), so every store instruction of a wave writes 64 consecutive bins
-// (512 B).  The segment's trackers are SEEDED exactly, not slid from the previous segment:
-// Y_m = FFT_N(x[w0 + i] e^{-j m th i}) in LDS (radix-2 Stockham, table twiddles) gives
+// Layout: one workgroup per segment of consecutive windows (32..256 windows, about two rounds of
+// resident workgroups: launch_t), N/(2B) threads; thread t owns bins k = 2 (t + NT q) + e (q < B/2,
+// e < 2), so every store instruction of a wave writes 128 consecutive bins (1 KiB fp64) as one 16-B
+// store per lane.  The segment's trackers are SEEDED exactly, not slid from the previous segment:
+// Y_m = FFT_N(x[w0 + i] e^{-j m th i}) in LDS (radix-4 Stockham, quarter twiddle table in LDS) gives
 // S(k/N + m phi) = Y_m[k] and S(k/N - m phi) = conj(Y_m[N-k]).  The per-step uniforms
-// (u_0, u_1, u_2, x[w+N] - x[w]) of the whole segment are staged in LDS, read by broadcast.
+// (u_0, u_1, u_2, x[w+N] - x[w]) are staged in LDS a chunk at a time and read by broadcast.
 // With the mean detrend the trackers follow the samples minus the segment's first sample.
-// Rounding: a tracker's error grows at most linearly over R <= 512 steps (~5e-14 of its own
-// magnitude); the parity bars are BASELINE.md 2's (tests/test_gpu_parity.py, test_gpu_fullgrid.py).
+// Rounding: a tracker's error grows at most linearly with the segment length (<= 256 steps by
+// default: ~3e-14 of its own magnitude); the parity bars are BASELINE.md 2's (tests/test_gpu_slide.py,
+// tests/test_gpu_fullgrid.py, the CPU model tests/test_slide_model.py).
+#include <atomic>
+
 #include "wsp_internal.h"
 
 namespace wsp {
@@ -35,19 +39,22 @@ namespace {
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kSlideB = 4;       // bins per thread
-constexpr int kSlideRMax = 512;  // windows per segment (LDS staging of the per-step uniforms)
+constexpr int kSlideRMax = 512;  // most steps whose uniforms are staged in LDS at once
 
 template <int NF> struct Rec { static constexpr int n = NF + 1; };  // [u0, (u1r, u1i), (u2r, u2i), d]
 
 __device__ __forceinline__ d2 cmul(d2 a, d2 b) { return d2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 
-// In-place natural-order complex FFT of N points in LDS (Stockham radix 2, DIT), NT threads,
-// twiddles W_N^k from the table (k < N/2).  Ends after a barrier.
-template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, const d2 *__restrict__ tw) {
-    constexpr int N = 1 << LOG2N, H = N / 2, Q = H / NT;
+// In-place natural-order complex FFT of N points in LDS: Stockham DIT, one radix-2 stage first when
+// log2 N is odd, then radix 4; NT threads.  twl[k] = W_N^k for k < N/4 (LDS, or the global table at
+// N = 8192 where LDS is full); a radix-4 butterfly loads W^k and forms W^2k, W^3k by products.
+// Ends after a barrier.
+template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, const d2 *twl) {
+    constexpr int N = 1 << LOG2N, H = N / 2, N4 = N / 4;
     const int t = threadIdx.x;
-    for (int s = 0; s < LOG2N; ++s) {
-        const int ns = 1 << s;
+    int ns = 1;
+    if constexpr (LOG2N & 1) {  // radix 2, Ns = 1: no twiddles
+        constexpr int Q = H / NT;
         d2 a[Q], b[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -57,26 +64,62 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, co
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
+            const int j = t + NT * q;
+            buf[2 * j] = a[q] + b[q];
+            buf[2 * j + 1] = a[q] - b[q];
+        }
+        __syncthreads();
+        ns = 2;
+    }
+    constexpr int Q = N4 / NT;
+#pragma unroll 1
+    for (; ns < N; ns *= 4) {
+        const int tws = N / (4 * ns);  // W_{4 Ns}^k = W_N^{k N/(4 Ns)}
+        d2 v[Q][4], w1[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = t + NT * q;
+            w1[q] = twl[(j & (ns - 1)) * tws];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * N4];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
             const int j = t + NT * q, k = j & (ns - 1);
-            const d2 bw = cmul(b[q], tw[k << (LOG2N - 1 - s)]);
-            const int d = ((j - k) << 1) + k;
-            buf[d] = a[q] + bw;
-            buf[d + ns] = a[q] - bw;
+            const d2 w2 = cmul(w1[q], w1[q]), w3 = cmul(w1[q], w2);
+            const d2 x1 = cmul(v[q][1], w1[q]), x2 = cmul(v[q][2], w2), x3 = cmul(v[q][3], w3);
+            const d2 t0 = v[q][0] + x2, t1 = v[q][0] - x2, t2 = x1 + x3, d = x1 - x3;
+            const d2 t3 = d2{d.y, -d.x};  // -i (x1 - x3)
+            const int o = ((j - k) << 2) + k;
+            buf[o] = t0 + t2;
+            buf[o + ns] = t1 + t3;
+            buf[o + 2 * ns] = t0 - t2;
+            buf[o + 3 * ns] = t1 - t3;
         }
         __syncthreads();
     }
 }
+
+// Bin b of thread t: pairs of adjacent bins, 2 (t + NT (b / 2)) + b % 2, so that a wave's store of a pair
+// of powers is one 16-B access per lane (1 KiB contiguous per wave instruction).
+template <int NT> __device__ __forceinline__ int kbin_of(int t, int b) { return 2 * (t + NT * (b >> 1)) + (b & 1); }
 
 template <typename T, int LOG2N, int NF, int DETREND>
 __global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 3 ? 3 : 4)) void slide_kernel(SlideArgs a) {
     constexpr int N = 1 << LOG2N, M = N / 2, B = kSlideB, NT = M / B;
     constexpr int NM = (NF - 1) / 2;  // modulations m = 1..NM
     constexpr int REC = Rec<NF>::n;
-    constexpr int LDS2 = (N > kSlideRMax * REC / 2) ? N : kSlideRMax * REC / 2;
+    // per-step uniforms staged CH steps at a time: N/4 clamped to [128, 512], so that small windows keep
+    // 4 single-/two-wave workgroups per SIMD (LDS: FFT buffer + quarter twiddles + uniforms)
+    constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
+    constexpr int LDS2 = (N > CH * REC / 2) ? N : CH * REC / 2;
+    constexpr bool TWL = N <= 4096;  // the quarter twiddle table fits LDS beside the FFT buffer
     __shared__ d2 lds[LDS2];
-    __shared__ double sum0;
+    __shared__ d2 twq[TWL ? N / 4 : 1];
 
     const int t = threadIdx.x;
+    auto kbin = [](int tt, int b) { return kbin_of<NT>(tt, b); };
     const int64_t w0 = (int64_t)blockIdx.x * a.seg;
     if (w0 >= a.n_windows) return;
     const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
@@ -92,6 +135,13 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 
     // out of the trackers near DC (20x smaller rounding at bins 0-2, tests/test_slide_model.py).
     const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
 
+    double sum0 = 0.0;
+    const d2 *twl = tw;
+    if constexpr (TWL) {
+        for (int i = t; i < N / 4; i += NT) twq[i] = tw[i];
+        twl = twq;
+    }
+
     // ---- seeds: trackers of window w0 from NM + 1 complex FFTs
 #pragma unroll
     for (int m = 0; m <= NM; ++m) {
@@ -100,11 +150,11 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 
             lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
         }
         __syncthreads();
-        fft_lds<LOG2N, NT>(lds, tw);
+        fft_lds<LOG2N, NT>(lds, twl);
         const double s = m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2);
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            const int k = t + NT * b;
+            const int k = kbin(t, b);
             if (m == 0) {
                 tr[b][0] = s * lds[k];
             } else {
@@ -113,84 +163,116 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 
                 tr[b][2 * m] = s * d2{ym.x, -ym.y};
             }
         }
-        if (DETREND == kDetrendMean && m == 0 && t == 0) sum0 = lds[0].x;
+        if (DETREND == kDetrendMean && m == 0) sum0 = lds[0].x;  // broadcast read: sum of x - L
         __syncthreads();
     }
-
-    // ---- per-step uniforms of the segment: u_m = s_m (x[w+N] e^{-j m th} - x[w]), d = x[w+N] - x[w]
-    double *u = reinterpret_cast<double *>(lds);
-    for (int st = t; st < len - 1; st += NT) {
-        const double xw = (double)x[st] - lvl, xn = (double)x[st + N] - lvl;
-        double *r = u + st * REC;
-        r[0] = a.s0 * (xn - xw);
-        if constexpr (NF >= 3) {
-            r[1] = a.s1 * (xn * a.c1 - xw);
-            r[2] = -(a.s1 * (xn * a.sn1));
-        }
-        if constexpr (NF >= 5) {
-            r[3] = a.s2 * (xn * a.c2 - xw);
-            r[4] = -(a.s2 * (xn * a.sn2));
-        }
-        r[REC - 1] = xn - xw;
-    }
-    __syncthreads();
 
 #pragma unroll
     for (int b = 0; b < B; ++b)
 #pragma unroll
-        for (int f = 0; f < NF; ++f) om[b][f] = omega[f * M + t + NT * b];
+        for (int f = 0; f < NF; ++f) om[b][f] = omega[f * M + kbin(t, b)];
     d2 hk[B];
     double sum = 0.0;
     if constexpr (DETREND == kDetrendMean) {
 #pragma unroll
-        for (int b = 0; b < B; ++b) hk[b] = hwin[t + NT * b];
+        for (int b = 0; b < B; ++b) hk[b] = hwin[kbin(t, b)];
         sum = sum0;
     }
 
-    // ---- slide
-    T *__restrict__ out = static_cast<T *>(a.out) + w0 * M + t;
-#pragma unroll 1
-    for (int st = 0; st < len; ++st) {
-        double mw = 0.0;
-        if constexpr (DETREND == kDetrendMean) mw = sum * a.inv_n;
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            d2 X = tr[b][0];
-#pragma unroll
-            for (int f = 1; f < NF; ++f) X += tr[b][f];
-            if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
-            const double p = X.x * X.x + X.y * X.y;
-            __builtin_nontemporal_store((T)p, out + NT * b);
-        }
-        out += M;
-        if (st + 1 < len) {
-            const double *r = u + st * REC;
-            const double u0 = r[0];
-#pragma unroll
-            for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
+    T *__restrict__ out = static_cast<T *>(a.out) + w0 * M + 2 * t;
+    double *u = reinterpret_cast<double *>(lds);
+    for (int c0 = 0; c0 < len; c0 += CH) {
+        const int clen = len - c0 < CH ? len - c0 : CH;
+        // ---- per-step uniforms of the chunk: u_m = s_m (x[w+N] e^{-j m th} - x[w]), d = x[w+N] - x[w]
+        if (c0) __syncthreads();  // the previous chunk's reads are done
+        for (int st = t; st < clen; st += NT) {
+            if (c0 + st + 1 >= len) break;  // no step after the last window
+            const double xw = (double)x[c0 + st] - lvl, xn = (double)x[c0 + st + N] - lvl;
+            double *r = u + st * REC;
+            r[0] = a.s0 * (xn - xw);
             if constexpr (NF >= 3) {
-                const double u1r = r[1], u1i = r[2];
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
-                    tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
-                }
+                r[1] = a.s1 * (xn * a.c1 - xw);
+                r[2] = -(a.s1 * (xn * a.sn1));
             }
             if constexpr (NF >= 5) {
-                const double u2r = r[3], u2i = r[4];
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
-                    tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
-                }
+                r[3] = a.s2 * (xn * a.c2 - xw);
+                r[4] = -(a.s2 * (xn * a.sn2));
             }
-            if constexpr (DETREND == kDetrendMean) sum += r[REC - 1];
+            r[REC - 1] = xn - xw;
+        }
+        __syncthreads();
+
+        // ---- slide
+#pragma unroll 1
+        for (int st = 0; st < clen; ++st) {
+            double mw = 0.0;
+            if constexpr (DETREND == kDetrendMean) mw = sum * a.inv_n;
+            double p[B];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                d2 X = tr[b][0];
+#pragma unroll
+                for (int f = 1; f < NF; ++f) X += tr[b][f];
+                if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
+                p[b] = X.x * X.x + X.y * X.y;
+            }
+            // bins 2(t + NT q) and 2(t + NT q) + 1: one 16-B (fp64) / 8-B (fp32) store per pair; plain
+            // stores: a pure write stream runs at 5.75 TB/s plain vs 5.5 non-temporal
+            // (tools/write_probe.hip, profiles/r02/slide/write_probe.log)
+#pragma unroll
+            for (int q = 0; q < B / 2; ++q) {
+                typedef T v2t __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)p[2 * q], (T)p[2 * q + 1]};
+            }
+            out += M;
+            if (c0 + st + 1 < len) {
+                const double *r = u + st * REC;
+                const double u0 = r[0];
+#pragma unroll
+                for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
+                if constexpr (NF >= 3) {
+                    const double u1r = r[1], u1i = r[2];
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
+                        tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
+                    }
+                }
+                if constexpr (NF >= 5) {
+                    const double u2r = r[3], u2i = r[4];
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
+                        tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
+                    }
+                }
+                if constexpr (DETREND == kDetrendMean) sum += r[REC - 1];
+            }
         }
     }
 }
 
-template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a, hipStream_t s) {
+// Workgroups: each slides a segment of consecutive windows (seeded once, per-step uniforms staged CH
+// steps at a time); segment length from the residency (occupancy API, once per instantiation).
+template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a0, hipStream_t s) {
     constexpr int NT = (1 << LOG2N) / (2 * kSlideB);
+    static std::atomic<int> resident{0};
+    int res = resident.load(std::memory_order_relaxed);
+    if (res == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slide_kernel<T, LOG2N, NF, DETREND>, NT, 0) !=
+                hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return hipErrorInvalidValue;
+        res = per_cu * cus > 0 ? per_cu * cus : 256;
+        resident.store(res, std::memory_order_relaxed);
+    }
+    SlideArgs a = a0;
+    if (a.seg <= 0) {  // ~2 rounds of resident workgroups, 32..256 windows each (sweep: DESIGN.md 4.5)
+        a.seg = (a.n_windows + 2 * (int64_t)res - 1) / (2 * (int64_t)res);
+        a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
+    }
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
     hipLaunchKernelGGL((slide_kernel<T, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a);
     return hipGetLastError();
@@ -223,17 +305,9 @@ template <typename T> hipError_t by_n(const SlideArgs &a, hipStream_t s) {
 
 }  // namespace
 
-int64_t slide_segment(int64_t n_windows) {
-    // ~2048 segments (2 workgroups per CU, ~5% seeding cost at R = 512), 64 <= R <= 512
-    int64_t r = (n_windows + 2047) / 2048;
-    if (r < 64) r = 64;
-    if (r > kSlideRMax) r = kSlideRMax;
-    return r;
-}
-
 hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {
     if (a.n_windows <= 0) return hipSuccess;
-    if (a.seg < 1 || a.seg > kSlideRMax || a.log2n < kSlideMinLog2N || a.log2n > kSlideMaxLog2N)
+    if (a.log2n < kSlideMinLog2N || a.log2n > kSlideMaxLog2N)
         return hipErrorInvalidValue;
     return a.f32 ? by_n<float>(a, s) : by_n<double>(a, s);
 }

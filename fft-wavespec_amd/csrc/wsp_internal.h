@@ -109,7 +109,7 @@ struct SlideArgs {
     const void *twiddle;  // N complex W_N^k (double) -- the seed FFTs
     const void *omega;    // slide table (double complex): [nf][N/2] e^{2 pi j f}, [N/2] H_k, [(nf-1)/2][N] e^{-j m th i}
     int64_t n_windows;
-    int64_t seg;          // windows per workgroup (slide_segment)
+    int64_t seg;          // windows per workgroup; 0 = the launcher's policy
     int log2n, nf, detrend;
     bool f32;
     double s0, s1, s2;    // a0, a1/2, a2/2
@@ -117,6 +117,5 @@ struct SlideArgs {
     double inv_n;
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
-int64_t slide_segment(int64_t n_windows);
 
 }  // namespace wsp

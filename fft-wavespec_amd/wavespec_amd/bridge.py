@@ -66,6 +66,7 @@ SIGNATURES = {
     "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
     "wsp_plan_set_algorithm": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_get_algorithm": (C.c_int32, [C.c_int64]),
+    "wsp_plan_set_slide_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -302,6 +303,10 @@ class Plan:
     def set_algorithm(self, algo: str) -> None:
         """wsp_plan_set_algorithm: "auto", "fft" or "slide" (hop = 1 seeded sliding DFT)."""
         _check("wsp_plan_set_algorithm", lib().wsp_plan_set_algorithm(self.handle, self.ALGOS[algo]))
+
+    def set_slide_segment(self, windows: int) -> None:
+        """Tuning: windows per sliding-DFT workgroup (0 = the library's policy)."""
+        _check("wsp_plan_set_slide_segment", lib().wsp_plan_set_slide_segment(self.handle, windows))
 
     def algorithm(self) -> str:
         """What the next execute runs: "fft" or "slide"."""

@@ -266,6 +266,9 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
 #define MTB_ALGO_FFT 1
 #define MTB_ALGO_SLIDE 2
 MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
+/* Tuning: windows per sliding-DFT workgroup (each seeds its trackers once);
+ * 0 = the library's policy.  MTB_BAD_ARGS for an unknown plan or windows < 0. */
+MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
 

@@ -5,8 +5,9 @@ kernel on the same device buffers.
 
 Bars: per window max_k|P - P_ref| / max_k P_ref <= 1e-10 (fp64), <= 1e-5 (fp32), and
 the same over the in-band bins [ceil(N/200), floor(N/18)] normalised by the band maximum.  Every
-window of each batch is checked, so every segment seam (segments of 64..512 windows, each seeded
-by its own FFTs) is covered.
+window of each batch is checked, so every segment seam (workgroups of 32..256 windows by default,
+each seeded by its own FFTs, per-step uniforms staged up to 512 steps at a time) is covered; forced
+segment lengths above the staging chunk cover the chunk seams.
 """
 import numpy as np
 import pytest
@@ -73,7 +74,7 @@ def test_slide_f32(gpu_session, n):
 
 @pytest.mark.parametrize("nwin", [1, 2, 63, 64, 65, 511, 512, 513, 4097])
 def test_slide_segment_seams(gpu_session, nwin):
-    """Batch sizes around the segment length (64 windows below 131072 windows) and a single window."""
+    """Batch sizes around the segment and staging-chunk lengths and a single window."""
     torch = pytest.importorskip("torch")
     n = 1024
     s = synth.random_walk(nwin + n - 1, seed=nwin)
@@ -85,17 +86,20 @@ def test_slide_segment_seams(gpu_session, nwin):
     plan.close()
 
 
-def test_slide_vs_fft_large_segments(gpu_session):
-    """300k windows (512-window segments): slide against the FFT kernel on the same buffer, every
-    window; the oracle on the windows around every 37th seam."""
+@pytest.mark.parametrize("seg", [0, 1366])
+def test_slide_vs_fft_large_segments(gpu_session, seg):
+    """The C4 batch (1,048,576 windows; default segments, or 1366-window segments = three 512-step
+    staging chunks each): slide against the FFT kernel on the same buffer, every window; the oracle on
+    the windows around every 37th 512-window boundary."""
     torch = pytest.importorskip("torch")
-    n, nwin = 2048, 300_000
+    n, nwin = 2048, 1_048_576
     dev = torch.device("cuda", 0)
     d_s = synth.random_walk_torch(nwin + n - 1, 17, dev)
     outs = {}
     for algo in ("fft", "slide"):
         plan = bridge.Plan(0, n, 1, nwin, "none", "hann")
         plan.set_algorithm(algo)
+        plan.set_slide_segment(seg)
         d_o = torch.empty(nwin * (n // 2), dtype=torch.float64, device=dev)
         plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
