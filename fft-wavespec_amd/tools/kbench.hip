@@ -311,6 +311,37 @@ int main(int argc, char **argv) {
         }
     }
     if (argc > 1 && std::string(argv[1]) == "out") return out_main(argc > 2 ? atoi(argv[2]) : 20);
+    if (argc > 1 && std::string(argv[1]) == "store") {  // kbench store [reps=20] [rounds=4]: NT vs plain power-row stores
+        const int reps = argc > 2 ? atoi(argv[2]) : 20, rounds = argc > 3 ? atoi(argv[3]) : 4;
+        const int64_t W = 65536;
+        const int n = 4096;
+        double *x, *out, *tw;
+        CK(hipMalloc(&x, W * n * 8));
+        CK(hipMalloc(&out, W * n / 2 * 8));
+        CK(hipMalloc(&tw, n * 16));
+        std::vector<double> h(2 * n);
+        for (int k = 0; k < n; ++k) {
+            long double a = -2.0L * 3.14159265358979323846264338327950288L * k / n;
+            h[2 * k] = (double)cosl(a), h[2 * k + 1] = (double)sinl(a);
+        }
+        CK(hipMemcpy(tw, h.data(), n * 16, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(fill_walk, dim3(4096), dim3(256), 0, 0, x, W * n);
+        hipStream_t s;
+        CK(hipStreamCreate(&s));
+        SpectrumLaunch L{};
+        L.series = x, L.out = out, L.twiddle = tw, L.window = 1, L.hop = n, L.n_windows = W, L.log2n = 12;
+        L.nt_mode = 1, L.grid = kDefaultGrid;
+        const double bytes = (double)W * n * 8 * 1.5;
+        for (int round = 0; round < rounds; ++round) {
+            const float a = time_variant<kDefaultVar | kVarNtLoad>(L, s, reps);
+            const float b = time_variant<(kDefaultVar & ~kVarNtStore) | kVarNtLoad>(L, s, reps);
+            const float c = time_variant<(kDefaultVar & ~kVarNtStore)>(L, s, reps);
+            printf("round %d  nt-store %7.1f us %6.0f GB/s | plain-store %7.1f us %6.0f GB/s | plain-store, cached loads %7.1f us %6.0f GB/s\n",
+                   round, a, bytes / a / 1e3, b, bytes / b / 1e3, c, bytes / c / 1e3);
+            fflush(stdout);
+        }
+        return 0;
+    }
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;
