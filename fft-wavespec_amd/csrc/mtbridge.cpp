@@ -35,7 +35,10 @@ namespace {
 using namespace wsp;
 
 // ------------------------------------------------------------- last error
-thread_local std::string t_last_error;
+// initial-exec: the 32-B string sits in the static TLS surplus even when the library is dlopen()ed, so no
+// __tls_get_addr allocation runs on a caller's first error (ThreadSanitizer's interceptor of that path
+// intermittently aborted the tests/hostsan stress driver with "unable to unmap")
+thread_local std::string t_last_error __attribute__((tls_model("initial-exec")));
 
 void set_error(const char *fmt, ...) {
     char buf[512];

@@ -230,6 +230,15 @@ hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t s) {
     return hipSuccess;
 }
 hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
+hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {  // hop = 1 power rows, same record function
+    const SlideArgs c = a;
+    run_on(s, [c] {
+        const int n = 1 << c.log2n;
+        if (c.f32) fill<float>(c.series, 1, n, c.n_windows, n / 2, c.out);
+        else fill<double>(c.series, 1, n, c.n_windows, n / 2, c.out);
+    });
+    return hipSuccess;
+}
 hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // detrended = the window itself
     const KalmanLaunch c = L;
