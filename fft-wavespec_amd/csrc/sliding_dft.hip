@@ -38,7 +38,9 @@ namespace {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-constexpr int kSlideB = 4;       // bins per thread
+// bins per thread: 4, or 2 for windows up to 1024 (C5's short-window plans: twice the threads per
+// workgroup for the same segment)
+template <int LOG2N> constexpr int slide_b() { return LOG2N <= 10 ? 2 : 4; }
 constexpr int kSlideRMax = 512;  // most steps whose uniforms are staged in LDS at once
 
 template <int NF> struct Rec { static constexpr int n = NF + 1; };  // [u0, (u1r, u1i), (u2r, u2i), d]
@@ -106,8 +108,9 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, co
 template <int NT> __device__ __forceinline__ int kbin_of(int t, int b) { return 2 * (t + NT * (b >> 1)) + (b & 1); }
 
 template <typename T, int LOG2N, int NF, int DETREND>
-__global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 3 ? 3 : 4)) void slide_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, M = N / 2, B = kSlideB, NT = M / B;
+__global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
+                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B;
     constexpr int NM = (NF - 1) / 2;  // modulations m = 1..NM
     constexpr int REC = Rec<NF>::n;
     // per-step uniforms staged CH steps at a time: N/4 clamped to [128, 512], so that small windows keep
@@ -255,7 +258,7 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * kSlideB), NF >= 5 ? 2 : (NF >= 
 // Workgroups: each slides a segment of consecutive windows (seeded once, per-step uniforms staged CH
 // steps at a time); segment length from the residency (occupancy API, once per instantiation).
 template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a0, hipStream_t s) {
-    constexpr int NT = (1 << LOG2N) / (2 * kSlideB);
+    constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
     static std::atomic<int> resident{0};
     int res = resident.load(std::memory_order_relaxed);
     if (res == 0) {
