@@ -100,8 +100,20 @@ template <typename T, int LOG2N, int VAR> constexpr bool band_fits(int span) {
            (span <= 64 * 8 && (int64_t)span * (int64_t)sizeof(cpx<T>) <= (int64_t)Geo<LOG2N>::SLOT * (int64_t)sizeof(T));
 }
 
+// Non-temporal sample loads as a compile-time variant (kVarNtLoad) where the windows do not overlap:
+// the run-time form (a.nt) costs the north-star kernel 4 % (539-540 vs 518 us per launch on one box,
+// kbench store mode, profiles/r02/kbench_ns_ntload.log).  Instantiated for the power and top-k outputs
+// at N >= 1024 without the IIR detrend; elsewhere a.nt still selects the loads at run time.
+template <typename T, int LOG2N, int DETREND, int OUT, int VAR> constexpr bool ct_nt_variant() {
+    return !(VAR & kVarNtLoad) && (OUT == kOutPower || OUT == kOutTopK) && LOG2N >= 10 && DETREND != kDetrendIir;
+}
+
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
 hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
+    if constexpr (ct_nt_variant<T, LOG2N, DETREND, OUT, VAR>()) {
+        if (L.nt_mode == 2 || (L.nt_mode == 0 && L.hop >= (int64_t(1) << LOG2N)))
+            return launch_one<T, LOG2N, DETREND, OUT, WCLASS, VAR | kVarNtLoad>(L, stream);
+    }
     using G = Blk<LOG2N, VAR>;
     const SpecArgs<T> a = make_args<T>(L, G::WPB);
     int64_t grid = L.grid > 0 ? L.grid : kDefaultGrid;
