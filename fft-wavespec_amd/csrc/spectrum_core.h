@@ -175,6 +175,7 @@ enum Var : int {
     kVarWinRec = 2048,  // Hann/Hamming values by a 3-term (Chebyshev) recurrence: 3 ops per sample, not 5
     kVarLdsB64 = 4096,  // with kVarSplitLds: exchange reads as single ds_read_b64 (no ds_read2_b64 pairing)
     kVarWinTab = 8192,  // window values (with the R2C factor 1/2) from an fp64 table a.win (L1/L2-resident)
+    kVarVec = 16384,    // sample pairs known 2-element aligned: one 16-B (8-B) load per pair, no run-time test of a.vec
 };
 
 // Workgroup shape of a variant: kVarWave1 shrinks the workgroup to one wave
@@ -715,7 +716,7 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
     using v2 = typename V2<T>::t;
     const int64_t w = g * Blk<LOG2N, VAR>::WPB + slot;
     const T *__restrict__ xw = a.series + (w < a.n_windows ? w : 0) * a.hop;
-    if (a.vec) {
+    if ((VAR & kVarVec) || a.vec) {
 #pragma unroll
         for (int q = 0; q < G::BPT0; ++q)
 #pragma unroll

@@ -336,11 +336,12 @@ int main(int argc, char **argv) {
             const float a = time_variant<kDefaultVar | kVarNtLoad>(L, s, reps);
             const float b = time_variant<(kDefaultVar & ~kVarNtStore) | kVarNtLoad>(L, s, reps);
             const float c = time_variant<(kDefaultVar & ~kVarNtStore)>(L, s, reps);
-            L.nt_mode = 2;  // the library's form: nt loads chosen at run time (a.nt, hop >= N)
+            L.nt_mode = 2;  // nt loads chosen at run time (a.nt, hop >= N): the round-2 library before ct_nt_variant
             const float d = time_variant<kDefaultVar>(L, s, reps);
             L.nt_mode = 1;
-            printf("round %d  nt-store %7.1f us %6.0f GB/s | plain-store %7.1f us %6.0f GB/s | plain-store, cached loads %7.1f us %6.0f GB/s | library (run-time nt loads) %7.1f us %6.0f GB/s\n",
-                   round, a, bytes / a / 1e3, b, bytes / b / 1e3, c, bytes / c / 1e3, d, bytes / d / 1e3);
+            const float e = time_variant<kDefaultVar | kVarNtLoad | kVarVec>(L, s, reps);
+            printf("round %d  nt-store %7.1f us %6.0f GB/s | plain-store %7.1f us %6.0f GB/s | plain-store, cached loads %7.1f us %6.0f GB/s | run-time nt loads %7.1f us %6.0f GB/s | nt + compile-time pair loads %7.1f us %6.0f GB/s\n",
+                   round, a, bytes / a / 1e3, b, bytes / b / 1e3, c, bytes / c / 1e3, d, bytes / d / 1e3, e, bytes / e / 1e3);
             fflush(stdout);
         }
         return 0;
