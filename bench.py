@@ -64,6 +64,9 @@ def parse(argv=None):
     ap.add_argument("--algo", default="auto", choices=["auto", "fft", "slide"],
                     help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
     ap.add_argument("--slide-seg", type=int, default=0, help="windows per sliding-DFT workgroup (0 = library policy)")
+    ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
+                    help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
+    ap.add_argument("--c5-streams", type=int, default=3, help="C5: streams the symbol plans are spread over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
@@ -349,7 +352,7 @@ class C5Batch(Workload):
     symbol).  One step = every owned symbol's batch; each window length runs on its own stream,
     joined into the launch stream."""
 
-    def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0):
+    def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0, c5_layout="greedy", c5_streams=3):
         import torch
         from wavespec_amd import bridge, synth
         dev = torch.device("cuda", local_rank)
@@ -359,14 +362,19 @@ class C5Batch(Workload):
         owned, seed_off = sp["symbols"], sp["seed_offset"]
         # Three streams, within the box's 4 HIP hardware queues together with the launch stream (with
         # one stream per length two of them shared a hardware queue and ran 14 kernels back to back:
-        # the whole step, profiles/r02/c5_kernel_stats.csv); symbols assigned to the
-        # least-loaded stream by windows x N log N (C5_LAYOUT=greedy) or by window length (default:
-        # {4096}, {2048}, {1024, 512}).  C5_STREAMS=1 puts every symbol on one stream (ablation).
-        nstreams = int(os.environ.get("C5_STREAMS", "3"))
+        # the whole step, profiles/r02/c5_kernel_stats.csv).  --c5-layout: "length" puts {4096}, {2048},
+        # {1024, 512} on their own streams; "greedy" assigns symbols longest-first to the least-loaded
+        # stream by output bytes (what the hop = 1 sliding DFT's time follows: nwin x N/2), "nlogn" the
+        # same by windows x N log N (the FFT kernel's work).  --c5-streams 1 runs every symbol on one
+        # stream (ablation).
+        nstreams = c5_streams
         self.streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
-        cost = {sym: nwins[sym] * lens[sym // 7] * int(np.log2(lens[sym // 7])) for sym in owned}
+        if c5_layout == "nlogn":
+            cost = {sym: nwins[sym] * lens[sym // 7] * int(np.log2(lens[sym // 7])) for sym in owned}
+        else:
+            cost = {sym: nwins[sym] * (lens[sym // 7] // 2) for sym in owned}
         load, assign = [0] * nstreams, {}
-        if os.environ.get("C5_LAYOUT", "length") == "greedy":
+        if c5_layout in ("greedy", "nlogn"):
             for sym in sorted(owned, key=lambda x: -cost[x]):
                 k = load.index(min(load))
                 assign[sym] = k
@@ -374,6 +382,8 @@ class C5Batch(Workload):
         else:  # by window length: {4096}, {2048}, {1024, 512}
             for sym in owned:
                 assign[sym] = {4096: 0, 2048: 1, 1024: 2, 512: 2}[lens[sym // 7]] % nstreams
+        self.layout = {"layout": c5_layout, "streams": nstreams,
+                       "stream_load": [sum(cost[x] for x in owned if assign[x] == k) for k in range(nstreams)]}
         self.jobs = []  # (plan, series, out, stream), launched longest first
         for sym in sorted(owned, key=lambda x: -cost[x]):
             n = lens[sym // 7]
@@ -438,7 +448,7 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     ctl = Control(world)
     if args.config == "c5":
-        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
+        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.c5_layout, args.c5_streams)
     else:
         wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
     torch.cuda.synchronize()
@@ -473,7 +483,7 @@ def main(argv=None):
             "data": "synthetic (random-walk close prices generated on device, seed per rank)",
             "config": {"workload": wl.describe, "windows_per_gpu": wl.windows, "windows_total": int(total_windows / args.steps),
                        "parallelism": f"windows sharded x{world} ({args.scaling}), no collective",
-                       "algorithm": wl.algorithm},
+                       "algorithm": wl.algorithm, **({"c5": wl.layout} if hasattr(wl, "layout") else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
                          "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,
