@@ -102,10 +102,10 @@ template <typename T, int LOG2N, int VAR> constexpr bool band_fits(int span) {
 
 // Non-temporal sample loads as a compile-time variant (kVarNtLoad) where the windows do not overlap:
 // the run-time form (a.nt) costs the north-star kernel 4 % (539-540 vs 518 us per launch on one box,
-// kbench store mode, profiles/r02/kbench_ns_ntload.log).  Instantiated for the power and top-k outputs
-// at N >= 1024 without the IIR detrend; elsewhere a.nt still selects the loads at run time.
+// kbench store mode, profiles/r02/kbench_ns_ntload.log).  Instantiated for every output but packed at
+// N >= 1024 without the IIR detrend; elsewhere a.nt still selects the loads at run time.
 template <typename T, int LOG2N, int DETREND, int OUT, int VAR> constexpr bool ct_nt_variant() {
-    return !(VAR & kVarNtLoad) && (OUT == kOutPower || OUT == kOutTopK) && LOG2N >= 10 && DETREND != kDetrendIir;
+    return !(VAR & kVarNtLoad) && OUT != kOutPacked && LOG2N >= 10 && DETREND != kDetrendIir;
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
