@@ -324,13 +324,22 @@ int ilog2_exact(int n) {
     return l;
 }
 
-// Device workspace of one launch: [detrended windows][per-window means][chunk column results]
+// Device workspace of one launch: [detrended windows][per-window means][chunk column results], or the
+// segment seeds of a hop = 1 top-k launch by the sliding DFT (its only workspace)
 struct WsLayout {
     size_t det = 0, means = 0, y = 0, total = 0;
 };
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+bool use_slide_topk(const Config &c);
+int64_t slide_topk_seg(const Config &c) { return c.slide_seg > 0 ? c.slide_seg : 128; }  // swept 32..256: 128 best
 WsLayout ws_layout(const Config &c) {
     WsLayout L;
+    if (use_slide_topk(c)) {
+        const int nf = window_coef(c.window).nf;
+        const int64_t nseg = (c.n_windows + slide_topk_seg(c) - 1) / slide_topk_seg(c);
+        L.total = (size_t)nseg * (size_t)slide_topk_seed_stride(nf, c.kmax - c.kmin + 1) * 2 * sizeof(double);
+        return L;
+    }
     const size_t es = c.elem();
     const bool large = c.op == kOpSpectrum && c.log2n > kMaxLog2N;
     size_t det = 0, means = 0, y = 0;
@@ -430,6 +439,18 @@ bool use_slide(const Config &c) {
     if (c.algo == MTB_ALGO_FFT || !slide_eligible(c)) return false;
     return c.algo == MTB_ALGO_SLIDE || c.n_windows >= 256;
 }
+// hop = 1 top-k records (MTB_OUT_TOPK, fp64) by the sliding DFT: only the band's bins are tracked (span <= 512)
+bool slide_topk_eligible(const Config &c) {
+    const int nf = window_coef(c.window).nf;
+    const int span = c.kmax - c.kmin + 1;
+    return c.op == kOpSpectrum && c.hop == 1 && c.output == MTB_OUT_TOPK && !c.f32 && c.log2n >= kSlideMinLog2N &&
+           c.log2n <= kSlideMaxLog2N && (c.detrend == MTB_DETREND_NONE || c.detrend == MTB_DETREND_MEAN) && nf > 0 &&
+           span >= 1 && span <= kSlideTopkMaxSpan;
+}
+bool use_slide_topk(const Config &c) {
+    if (c.algo == MTB_ALGO_FFT || !slide_topk_eligible(c)) return false;
+    return c.algo == MTB_ALGO_SLIDE || c.n_windows >= 256;
+}
 
 // ------------------------------------------------------------ device path
 // series (device) -> [Kalman pre-pass into ws] -> spectrum kernel -> out.
@@ -488,7 +509,8 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         HIP_OR(launch_large(G, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
-    if (use_slide(c)) {
+    if (use_slide(c) || use_slide_topk(c)) {
+        const bool topk = use_slide_topk(c);
         Tables t64;
         void *stab = nullptr;
         if ((st = get_tables(dev, c.log2n, false, &t64)) != MTB_OK) return st;
@@ -510,6 +532,15 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         A.s0 = wc.a0, A.s1 = wc.a1 / 2, A.s2 = wc.a2 / 2;
         A.c1 = (double)cosl(th), A.sn1 = (double)sinl(th), A.c2 = (double)cosl(2 * th), A.sn2 = (double)sinl(2 * th);
         A.inv_n = 1.0 / c.n;
+        if (topk) {
+            A.seg = slide_topk_seg(c);
+            A.kmin = c.kmin;
+            A.span = c.kmax - c.kmin + 1;
+            A.topk = c.topk;
+            A.ws = d_ws;
+            HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
+            return MTB_OK;
+        }
         HIP_OR(launch_slide(A, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
@@ -900,21 +931,39 @@ void release_jobs(bool all, std::thread::id owner) {
 // a concurrent wsp_plan_destroy cannot free the workspace under it (the last
 // reference frees it, after the device has finished with it), and cfg is
 // read and written under the plan's own mutex (wsp_plan_set_topk).
+// The workspace is a shared_ptr: an execute holds the one it enqueued with, so a reconfiguration that
+// needs a larger one (wsp_plan_set_topk / _set_algorithm / _set_slide_segment) swaps it without freeing
+// memory a queued launch still uses (the last holder frees it after the device has finished).
 struct Plan {
     int dev = 0;
     std::mutex mu;
     Config cfg;
     double kalman[16];
-    void *d_ws = nullptr;
+    std::shared_ptr<void> ws;
     size_t ws_bytes = 0;
-    ~Plan() {
-        if (d_ws) {
-            (void)hipSetDevice(dev);
-            (void)hipDeviceSynchronize();
-            (void)hipFree(d_ws);
-        }
-    }
 };
+std::shared_ptr<void> plan_ws_alloc(int dev, size_t bytes) {
+    void *d = nullptr;
+    if (hipSetDevice(dev) != hipSuccess || hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+    return std::shared_ptr<void>(d, [dev](void *q) {
+        (void)hipSetDevice(dev);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(q);
+    });
+}
+// (under p->mu) grow the workspace to what cfg needs
+int plan_ws_fit(Plan &p) {
+    const size_t need = ws_layout(p.cfg).total;
+    if (need <= p.ws_bytes) return MTB_OK;
+    auto w = plan_ws_alloc(p.dev, need);
+    if (!w) {
+        set_error("hipMalloc(%zu) for the plan workspace failed", need);
+        return MTB_NO_MEM;
+    }
+    p.ws = std::move(w);
+    p.ws_bytes = need;
+    return MTB_OK;
+}
 std::mutex g_plans_mu;
 std::map<int64_t, std::shared_ptr<Plan>> *g_plans = new std::map<int64_t, std::shared_ptr<Plan>>();
 
@@ -1445,14 +1494,7 @@ MTB_API int64_t wsp_plan_create(int32_t device, int32_t window_len, int64_t hop,
     }
     Tables t;
     if (get_tables(device, p->cfg.log2n, p->cfg.f32, &t) != MTB_OK) return 0;
-    p->ws_bytes = ws_layout(p->cfg).total;
-    if (p->ws_bytes) {
-        if (hipSetDevice(device) != hipSuccess || hipMalloc(&p->d_ws, p->ws_bytes) != hipSuccess) {
-            p->d_ws = nullptr;
-            set_error("hipMalloc(%zu) for the plan workspace failed", p->ws_bytes);
-            return 0;
-        }
-    }
+    if (plan_ws_fit(*p) != MTB_OK) return 0;
     return plan_register(std::move(p));
 }
 
@@ -1484,11 +1526,13 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
         return MTB_BAD_ARGS;
     }
     Config c;
+    std::shared_ptr<void> ws;
     {
         std::lock_guard<std::mutex> lk(p->mu);
         c = p->cfg;
+        ws = p->ws;
     }
-    return enqueue(p->dev, c, p->kalman, d_series, d_out, p->d_ws, (hipStream_t)hip_stream);
+    return enqueue(p->dev, c, p->kalman, d_series, d_out, ws.get(), (hipStream_t)hip_stream);
 }
 
 MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period) {
@@ -1504,8 +1548,12 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
     }
     Config c = p->cfg;  // applied only when valid
     const int st = config_set_topk(&c, top_k, min_period, max_period);
-    if (st == MTB_OK) p->cfg = c;
-    return st;
+    if (st != MTB_OK) return st;
+    const Config old = p->cfg;
+    p->cfg = c;
+    const int sw = plan_ws_fit(*p);
+    if (sw != MTB_OK) p->cfg = old;
+    return sw;
 }
 
 MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
@@ -1521,13 +1569,16 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
     }
     Config c = p->cfg;
     c.algo = algo;
-    if (algo == MTB_ALGO_SLIDE && !slide_eligible(c)) {
+    if (algo == MTB_ALGO_SLIDE && !slide_eligible(c) && !slide_topk_eligible(c)) {
         set_error("plan %lld: the sliding DFT takes hop = 1, N = 512..8192, detrend none/mean, a cosine window "
-                  "and power output", (long long)plan);
+                  "and power output (or fp64 top-k records over at most 512 bins)", (long long)plan);
         return MTB_BAD_ARGS;
     }
+    const Config old = p->cfg;
     p->cfg = c;
-    return MTB_OK;
+    const int sw = plan_ws_fit(*p);
+    if (sw != MTB_OK) p->cfg = old;
+    return sw;
 }
 
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
@@ -1538,15 +1589,18 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);
+    const Config old = p->cfg;
     p->cfg.slide_seg = windows;
-    return MTB_OK;
+    const int sw = plan_ws_fit(*p);
+    if (sw != MTB_OK) p->cfg = old;
+    return sw;
 }
 
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan) {
     std::shared_ptr<Plan> p = find_plan(plan);
     if (!p) return MTB_BAD_ARGS;
     std::lock_guard<std::mutex> lk(p->mu);
-    return use_slide(p->cfg) ? MTB_ALGO_SLIDE : MTB_ALGO_FFT;
+    return (use_slide(p->cfg) || use_slide_topk(p->cfg)) ? MTB_ALGO_SLIDE : MTB_ALGO_FFT;
 }
 
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan) {

@@ -31,6 +31,7 @@
 // tests/test_gpu_fullgrid.py, the CPU model tests/test_slide_model.py).
 #include <atomic>
 
+#include "spectrum_core.h"  // topk_wave64: the one-wave top-k scan of the FFT kernel
 #include "wsp_internal.h"
 
 namespace wsp {
@@ -107,11 +108,86 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, co
 // of powers is one 16-B access per lane (1 KiB contiguous per wave instruction).
 template <int NT> __device__ __forceinline__ int kbin_of(int t, int b) { return 2 * (t + NT * (b >> 1)) + (b & 1); }
 
+// The segment's seeds: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}), m = 0 .. (NF-1)/2, in LDS; pick(m, s_m, Y)
+// takes what it needs from each transform (every thread calls it between the transform's barriers).
+template <typename T, int LOG2N, int NF, int DETREND, int NT, typename PICK>
+__device__ __forceinline__ void seed_ffts(const SlideArgs &a, const T *__restrict__ x, double lvl, d2 *lds, d2 *twq,
+                                          PICK pick) {
+    constexpr int N = 1 << LOG2N, M = N / 2, NM = (NF - 1) / 2;
+    constexpr bool TWL = N <= 4096;  // the quarter twiddle table fits LDS beside the FFT buffer
+    const int t = threadIdx.x;
+    const d2 *__restrict__ tw = static_cast<const d2 *>(a.twiddle);
+    const d2 *__restrict__ mod = static_cast<const d2 *>(a.omega) + (NF + 1) * M;  // [NM][N]
+    const d2 *twl = tw;
+    if constexpr (TWL) {
+        for (int i = t; i < N / 4; i += NT) twq[i] = tw[i];
+        twl = twq;
+    }
+#pragma unroll
+    for (int m = 0; m <= NM; ++m) {
+        for (int i = t; i < N; i += NT) {
+            const double xi = (double)x[i] - lvl;
+            lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
+        }
+        __syncthreads();
+        fft_lds<LOG2N, NT>(lds, twl);
+        pick(m, m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2), lds);
+        __syncthreads();
+    }
+}
+
+// Per-step uniforms of steps c0 .. c0 + clen - 1 into u[st * REC]: u_m = s_m (x[w+N] e^{-j m th} - x[w]),
+// d = x[w+N] - x[w] (samples minus the segment's level L); no step after the segment's last window.
+template <typename T, int NF, int N>
+__device__ __forceinline__ void stage_uniforms(const SlideArgs &a, const T *__restrict__ x, double lvl, int c0,
+                                               int clen, int len, double *u, int t, int nt) {
+    constexpr int REC = Rec<NF>::n;
+    for (int st = t; st < clen; st += nt) {
+        if (c0 + st + 1 >= len) break;
+        const double xw = (double)x[c0 + st] - lvl, xn = (double)x[c0 + st + N] - lvl;
+        double *r = u + st * REC;
+        r[0] = a.s0 * (xn - xw);
+        if constexpr (NF >= 3) {
+            r[1] = a.s1 * (xn * a.c1 - xw);
+            r[2] = -(a.s1 * (xn * a.sn1));
+        }
+        if constexpr (NF >= 5) {
+            r[3] = a.s2 * (xn * a.c2 - xw);
+            r[4] = -(a.s2 * (xn * a.sn2));
+        }
+        r[REC - 1] = xn - xw;
+    }
+}
+
+// One slide of B bins' trackers: T_f <- omega_f (T_f + u_m); the mean path's running sum of x - L.
+template <int B, int NF, int DETREND>
+__device__ __forceinline__ void slide_step(d2 (&tr)[B][NF], const d2 (&om)[B][NF], const double *r, double &sum) {
+    const double u0 = r[0];
+#pragma unroll
+    for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
+    if constexpr (NF >= 3) {
+        const double u1r = r[1], u1i = r[2];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
+            tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
+        }
+    }
+    if constexpr (NF >= 5) {
+        const double u2r = r[3], u2i = r[4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
+            tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
+        }
+    }
+    if constexpr (DETREND == kDetrendMean) sum += r[Rec<NF>::n - 1];
+}
+
 template <typename T, int LOG2N, int NF, int DETREND>
 __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
                              slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a) {
     constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B;
-    constexpr int NM = (NF - 1) / 2;  // modulations m = 1..NM
     constexpr int REC = Rec<NF>::n;
     // per-step uniforms staged CH steps at a time: N/4 clamped to [128, 512], so that small windows keep
     // 4 single-/two-wave workgroups per SIMD (LDS: FFT buffer + quarter twiddles + uniforms)
@@ -127,10 +203,8 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
     if (w0 >= a.n_windows) return;
     const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
     const T *__restrict__ x = static_cast<const T *>(a.series) + w0;
-    const d2 *__restrict__ tw = static_cast<const d2 *>(a.twiddle);
     const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);  // [NF][M]
     const d2 *__restrict__ hwin = omega + NF * M;                      // [M]
-    const d2 *__restrict__ mod = hwin + M;                             // [NM][N]
 
     d2 om[B][NF], tr[B][NF];
     // mean detrend: the trackers follow x - L, L = the segment's first sample, and the output subtracts
@@ -139,36 +213,20 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
     const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
 
     double sum0 = 0.0;
-    const d2 *twl = tw;
-    if constexpr (TWL) {
-        for (int i = t; i < N / 4; i += NT) twq[i] = tw[i];
-        twl = twq;
-    }
-
-    // ---- seeds: trackers of window w0 from NM + 1 complex FFTs
-#pragma unroll
-    for (int m = 0; m <= NM; ++m) {
-        for (int i = t; i < N; i += NT) {
-            const double xi = (double)x[i] - lvl;
-            lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
-        }
-        __syncthreads();
-        fft_lds<LOG2N, NT>(lds, twl);
-        const double s = m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2);
+    seed_ffts<T, LOG2N, NF, DETREND, NT>(a, x, lvl, lds, twq, [&](int m, double s, const d2 *y) {
 #pragma unroll
         for (int b = 0; b < B; ++b) {
             const int k = kbin(t, b);
             if (m == 0) {
-                tr[b][0] = s * lds[k];
+                tr[b][0] = s * y[k];
             } else {
-                const d2 yp = lds[k], ym = lds[(N - k) & (N - 1)];
+                const d2 yp = y[k], ym = y[(N - k) & (N - 1)];
                 tr[b][2 * m - 1] = s * yp;
                 tr[b][2 * m] = s * d2{ym.x, -ym.y};
             }
         }
-        if (DETREND == kDetrendMean && m == 0) sum0 = lds[0].x;  // broadcast read: sum of x - L
-        __syncthreads();
-    }
+        if (DETREND == kDetrendMean && m == 0) sum0 = y[0].x;  // broadcast read: sum of x - L
+    });
 
 #pragma unroll
     for (int b = 0; b < B; ++b)
@@ -186,23 +244,8 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
     double *u = reinterpret_cast<double *>(lds);
     for (int c0 = 0; c0 < len; c0 += CH) {
         const int clen = len - c0 < CH ? len - c0 : CH;
-        // ---- per-step uniforms of the chunk: u_m = s_m (x[w+N] e^{-j m th} - x[w]), d = x[w+N] - x[w]
         if (c0) __syncthreads();  // the previous chunk's reads are done
-        for (int st = t; st < clen; st += NT) {
-            if (c0 + st + 1 >= len) break;  // no step after the last window
-            const double xw = (double)x[c0 + st] - lvl, xn = (double)x[c0 + st + N] - lvl;
-            double *r = u + st * REC;
-            r[0] = a.s0 * (xn - xw);
-            if constexpr (NF >= 3) {
-                r[1] = a.s1 * (xn * a.c1 - xw);
-                r[2] = -(a.s1 * (xn * a.sn1));
-            }
-            if constexpr (NF >= 5) {
-                r[3] = a.s2 * (xn * a.c2 - xw);
-                r[4] = -(a.s2 * (xn * a.sn2));
-            }
-            r[REC - 1] = xn - xw;
-        }
+        stage_uniforms<T, NF, N>(a, x, lvl, c0, clen, len, u, t, NT);
         __syncthreads();
 
         // ---- slide
@@ -228,35 +271,131 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
                 *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)p[2 * q], (T)p[2 * q + 1]};
             }
             out += M;
-            if (c0 + st + 1 < len) {
-                const double *r = u + st * REC;
-                const double u0 = r[0];
-#pragma unroll
-                for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
-                if constexpr (NF >= 3) {
-                    const double u1r = r[1], u1i = r[2];
-#pragma unroll
-                    for (int b = 0; b < B; ++b) {
-                        tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
-                        tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
-                    }
-                }
-                if constexpr (NF >= 5) {
-                    const double u2r = r[3], u2i = r[4];
-#pragma unroll
-                    for (int b = 0; b < B; ++b) {
-                        tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
-                        tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
-                    }
-                }
-                if constexpr (DETREND == kDetrendMean) sum += r[REC - 1];
-            }
+            if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
         }
     }
 }
 
 // Workgroups: each slides a segment of consecutive windows (seeded once, per-step uniforms staged CH
 // steps at a time); segment length from the residency (occupancy API, once per instantiation).
+// ---- hop = 1 top-k records (MTB_OUT_TOPK): only the band's bins are tracked.
+// Seeds of every segment into the workspace: [NF][span] trackers of bins kmin .. kmin + span - 1, then
+// {sum of x - L (mean path), L}; one workgroup per segment, the same in-LDS FFTs as slide_kernel.
+template <typename T, int LOG2N, int NF, int DETREND>
+__global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>())) void slide_seed_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, NT = N / (2 * slide_b<LOG2N>());
+    constexpr bool TWL = N <= 4096;
+    __shared__ d2 lds[N];
+    __shared__ d2 twq[TWL ? N / 4 : 1];
+    const int t = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const T *__restrict__ x = static_cast<const T *>(a.series) + w0;
+    const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
+    d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int span = a.span, kmin = a.kmin;
+    seed_ffts<T, LOG2N, NF, DETREND, NT>(a, x, lvl, lds, twq, [&](int m, double s, const d2 *y) {
+        for (int j = t; j < span; j += NT) {
+            const int k = kmin + j;
+            if (m == 0) {
+                ws[j] = s * y[k];
+            } else {
+                const d2 ym = y[(N - k) & (N - 1)];
+                ws[(2 * m - 1) * span + j] = s * y[k];
+                ws[(2 * m) * span + j] = s * d2{ym.x, -ym.y};
+            }
+        }
+        if (m == 0 && t == 0) ws[NF * span] = d2{y[0].x, lvl};
+    });
+}
+
+// One wave per segment: lane l tracks bins kmin + l + 64 b (b < NB), stages each window's band X in LDS
+// and runs the FFT kernel's one-wave scan (core::topk_wave64: power desc, bin asc, as the reference's
+// strict-'>' insertion, L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554), which writes the
+// window's record row.
+template <int LOG2N, int NF, int DETREND, int NB>
+__global__ __launch_bounds__(64) void slide_topk_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128;
+    __shared__ double u[CHT * REC];
+    __shared__ core::cpx<double> xb[64 * NB];
+    const int l = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
+    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
+    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
+    const d2 *__restrict__ hwin = omega + NF * M;
+    const d2 *__restrict__ ws = static_cast<const d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int span = a.span, kmin = a.kmin;
+    d2 tr[NB][NF], om[NB][NF], hk[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = l + 64 * b;
+        const bool ok = j < span;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            tr[b][f] = ok ? ws[f * span + j] : d2{0.0, 0.0};
+            om[b][f] = ok ? omega[f * M + kmin + j] : d2{1.0, 0.0};
+        }
+        hk[b] = (DETREND == kDetrendMean && ok) ? hwin[kmin + j] : d2{0.0, 0.0};
+    }
+    const d2 sl = ws[NF * span];
+    double sum = sl.x;
+    const double lvl = sl.y;
+    double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
+    for (int c0 = 0; c0 < len; c0 += CHT) {
+        const int clen = len - c0 < CHT ? len - c0 : CHT;
+        if (c0) __syncthreads();
+        stage_uniforms<double, NF, N>(a, x, lvl, c0, clen, len, u, l, 64);
+        __syncthreads();
+#pragma unroll 1
+        for (int st = 0; st < clen; ++st) {
+            const double mw = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                d2 X = tr[b][0];
+#pragma unroll
+                for (int f = 1; f < NF; ++f) X += tr[b][f];
+                if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
+                xb[l + 64 * b] = core::cpx<double>{X.x, X.y};
+            }
+            __syncthreads();  // one wave: orders the band's LDS writes before the scan's reads
+            core::topk_wave64<NB, double>(xb, kmin, span, a.topk, l, rec, true);
+            __syncthreads();  // the scan's reads before the next window's writes
+            rec += 4 * a.topk;
+            if (c0 + st + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
+        }
+    }
+}
+
+template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
+    constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
+    const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
+    hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int nb = (a.span + 63) / 64;
+    if (nb <= 1) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 1>), dim3((unsigned)grid), dim3(64), 0, s, a);
+    else if (nb <= 2) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 2>), dim3((unsigned)grid), dim3(64), 0, s, a);
+    else if (nb <= 4) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 4>), dim3((unsigned)grid), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 8>), dim3((unsigned)grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int LOG2N, int NF> hipError_t topk_by_detrend(const SlideArgs &a, hipStream_t s) {
+    return a.detrend == kDetrendMean ? launch_topk_t<LOG2N, NF, kDetrendMean>(a, s)
+                                     : launch_topk_t<LOG2N, NF, kDetrendNone>(a, s);
+}
+
+template <int LOG2N> hipError_t topk_by_nf(const SlideArgs &a, hipStream_t s) {
+    switch (a.nf) {
+    case 1: return topk_by_detrend<LOG2N, 1>(a, s);
+    case 3: return topk_by_detrend<LOG2N, 3>(a, s);
+    case 5: return topk_by_detrend<LOG2N, 5>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a0, hipStream_t s) {
     constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
     static std::atomic<int> resident{0};
@@ -307,6 +446,21 @@ template <typename T> hipError_t by_n(const SlideArgs &a, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {
+    if (a.n_windows <= 0) return hipSuccess;
+    if (a.f32 || a.seg < 1 || a.span < 1 || a.span > kSlideTopkMaxSpan || a.kmin < 0 || a.kmin + a.span > (1 << a.log2n) / 2 ||
+        a.topk < 1 || a.topk > 64 || !a.ws)
+        return hipErrorInvalidValue;
+    switch (a.log2n) {
+    case 9: return topk_by_nf<9>(a, s);
+    case 10: return topk_by_nf<10>(a, s);
+    case 11: return topk_by_nf<11>(a, s);
+    case 12: return topk_by_nf<12>(a, s);
+    case 13: return topk_by_nf<13>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {
     if (a.n_windows <= 0) return hipSuccess;

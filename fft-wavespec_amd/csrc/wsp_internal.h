@@ -115,7 +115,15 @@ struct SlideArgs {
     double s0, s1, s2;    // a0, a1/2, a2/2
     double c1, sn1, c2, sn2;  // cos / sin of th and 2 th, th = 2 pi/(N-1)
     double inv_n;
+    // top-k records (launch_slide_topk, fp64): bins [kmin, kmin + span), topk slots, seeds workspace
+    int kmin, span, topk;
+    void *ws;             // ceil(n_windows / seg) * slide_topk_seed_stride(nf, span) double complex
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
+// hop = 1 top-k records ([bin, power, Re, Im] x topk per window, MTB_OUT_TOPK) by the sliding DFT: the
+// band's trackers only (span <= 512), one wave per segment, the FFT kernel's one-wave scan per window.
+constexpr int kSlideTopkMaxSpan = 512;
+__host__ __device__ inline int64_t slide_topk_seed_stride(int nf, int span) { return (int64_t)nf * span + 1; }
+hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t stream);
 
 }  // namespace wsp

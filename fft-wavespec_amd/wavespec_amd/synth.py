@@ -46,6 +46,9 @@ CONFIGS = {
     # spectrum and the inverse transform
     "ns_topk": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann", seed=11,
                     output="topk"),
+    # C4's batch reduced on device to the reference's top-8 scan (SURVEY 8f rank 1 on the hop = 1 shape)
+    "c4_topk": dict(windows=1048576, n=2048, hop=1, precision="f64", detrend="none", window="hann", seed=13,
+                    output="topk"),
     "ns_phase": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann", seed=11,
                      output="phase"),
     "ns_topk_phase": dict(windows=65536, n=4096, hop=4096, precision="f64", detrend="none", window="hann",

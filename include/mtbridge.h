@@ -258,7 +258,8 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
 /* Algorithm for hop = 1 batches (an extension; the reference always runs an
  * FFT per window).  MTB_ALGO_AUTO (default): the seeded sliding DFT when the
  * plan is eligible -- hop = 1, window_len 512..8192, detrend none or mean,
- * Hann / Hamming / Blackman / no window, MTB_OUT_POWER -- and has at least 256
+ * Hann / Hamming / Blackman / no window, MTB_OUT_POWER or fp64 MTB_OUT_TOPK over
+ * at most 512 bins -- and has at least 256
  * windows, otherwise the per-window FFT.  MTB_ALGO_FFT / MTB_ALGO_SLIDE force
  * one (MTB_BAD_ARGS if the plan is not eligible for the slide).  Both produce
  * the same spectra within the parity bars. */

@@ -230,6 +230,11 @@ hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t s) {
     return hipSuccess;
 }
 hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
+hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {  // hop = 1 top-k records, same record function
+    const SlideArgs c = a;
+    run_on(s, [c] { fill<double>(c.series, 1, 1 << c.log2n, c.n_windows, 4 * c.topk, c.out); });
+    return hipSuccess;
+}
 hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {  // hop = 1 power rows, same record function
     const SlideArgs c = a;
     run_on(s, [c] {

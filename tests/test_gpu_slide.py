@@ -179,3 +179,119 @@ def test_slide_host_batch_path(gpu_session):
     got = bridge.spectrum_batch(s, n, 1, "mean", "hamming")
     want = oracle.batch_spectrum(s, n, 1, "mean", "hamming")
     _bars(got, want, n, 1e-10)
+
+
+# ------------------------------------------------------------------ hop = 1 top-k records
+def _topk_run(n, nwin, s, detrend, window, k, pmin, pmax, algo, torch, seg=0):
+    plan = bridge.Plan(0, n, 1, nwin, detrend, window, output="topk")
+    plan.set_topk(k, pmin, pmax)
+    plan.set_algorithm(algo)
+    if seg:
+        plan.set_slide_segment(seg)
+    assert plan.algorithm() == algo
+    got = _run(plan, s, torch).reshape(nwin, k, 4)
+    plan.close()
+    return got
+
+
+def _topk_bars(got, want, spec_band_max, max_swaps):
+    """Bins identical up to rank swaps between near-equal powers; every slot's power within 1e-10 of
+    the window's in-band maximum; Re/Im of matching slots within 1e-10 of its square root."""
+    same = got[:, :, 0] == want[:, :, 0]
+    assert int((~same).sum()) <= max_swaps, int((~same).sum())
+    tol = 1e-10 * spec_band_max[:, None]
+    assert np.all(np.abs(got[:, :, 1] - want[:, :, 1]) <= tol)
+    amp = 1e-10 * np.sqrt(spec_band_max)[:, None]
+    assert np.all(np.abs(np.where(same, got[:, :, 2] - want[:, :, 2], 0.0)) <= amp)
+    assert np.all(np.abs(np.where(same, got[:, :, 3] - want[:, :, 3], 0.0)) <= amp)
+
+
+@pytest.mark.parametrize("n", [512, 1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("window,detrend", [("hann", "none"), ("blackman", "mean"), ("none", "none"),
+                                            ("hamming", "mean")])
+def test_slide_topk_matches_oracle(gpu_session, n, window, detrend):
+    """hop = 1 top-8 records over periods [18, 200] (the reference's scan, 1.1.0:22-23) by the sliding DFT
+    against the oracle's ora_batch_topk, every window."""
+    torch = pytest.importorskip("torch")
+    nwin = 1200 + n // 16
+    s = synth.random_walk(nwin + n - 1, seed=n + 3)
+    got = _topk_run(n, nwin, s, detrend, window, 8, 18.0, 200.0, "slide", torch)
+    want = oracle.batch_topk(s, n, 1, detrend, window, 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, detrend, window)
+    kmin, kmax = oracle.band(n)
+    _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
+@pytest.mark.parametrize("k,pmin,pmax", [(1, 18.0, 200.0), (64, 18.0, 200.0), (8, 4.0, 2000.0), (8, 100.0, 110.0),
+                                         (8, 4.1, 9.0)])
+def test_slide_topk_slots_and_bands(gpu_session, k, pmin, pmax):
+    """k = 1 and 64 slots, bands of 512 / 1-2 / ~250 bins (one to eight bins per lane), empty slots when
+    the band holds fewer bins than k; segments of 100 windows (ragged seams)."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 2048, 1000
+    s = synth.random_walk(nwin + n - 1, seed=k)
+    got = _topk_run(n, nwin, s, "none", "hann", k, pmin, pmax, "slide", torch, seg=100)
+    want = oracle.batch_topk(s, n, 1, "none", "hann", 0, None, k, pmin, pmax)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = int(np.ceil(n / pmax)), min(int(np.floor(n / pmin)), n // 2 - 1)
+    _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=8 if k == 64 else 2)
+
+
+def test_slide_topk_vs_fft_c4(gpu_session):
+    """C4's batch (1,048,576 windows x 2048) as top-8 records: sliding DFT against the FFT kernel's fused
+    scan on the same device buffer, every window."""
+    torch = pytest.importorskip("torch")
+    n, nwin, k = 2048, 1_048_576, 8
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(nwin + n - 1, 13, dev)
+    outs = {}
+    for algo in ("fft", "slide"):
+        plan = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+        plan.set_topk(k, 18.0, 200.0)
+        plan.set_algorithm(algo)
+        d_o = torch.empty(nwin * 4 * k, dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs[algo] = d_o.view(nwin, k, 4)
+        plan.close()
+    A, B = outs["slide"], outs["fft"]
+    same = A[:, :, 0] == B[:, :, 0]
+    assert int((~same).sum().item()) <= 64  # rank swaps between near-equal powers only
+    top = B[:, 0, 1]
+    assert ((A[:, :, 1] - B[:, :, 1]).abs() <= 1e-10 * top[:, None]).all().item()
+
+
+def test_slide_topk_workspace_follows_reconfiguration(gpu_session):
+    """A hop = 1 power plan switched to top-k records (wsp_plan_set_topk) and to shorter segments
+    (wsp_plan_set_slide_segment) grows its workspace for the seeds; results stay right."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 1024, 3000
+    s = synth.random_walk(nwin + n - 1, seed=77)
+    plan = bridge.Plan(0, n, 1, nwin, "none", "hann")
+    assert plan.algorithm() == "slide"
+    p0 = _run(plan, s, torch)
+    _bars(p0, oracle.batch_spectrum(s, n, 1, "none", "hann"), n, 1e-10)
+    plan.set_topk(8, 18.0, 200.0)
+    plan.output = "topk"
+    assert plan.algorithm() == "slide"
+    want = oracle.batch_topk(s, n, 1, "none", "hann", 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = oracle.band(n)
+    for seg in (0, 33, 1):
+        plan.set_slide_segment(seg)
+        got = _run(plan, s, torch).reshape(nwin, 8, 4)
+        _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+    plan.close()
+
+
+def test_slide_topk_refusals(gpu_session):
+    """fp32 plans and bands wider than 512 bins keep the FFT kernel's scan."""
+    p = bridge.Plan(0, 4096, 1, 4096, "none", "hann", 0, "f32", output="topk")
+    assert p.algorithm() == "fft"
+    p.close()
+    p = bridge.Plan(0, 4096, 1, 4096, "none", "hann", output="topk")
+    p.set_topk(8, 2.0, 4000.0)  # bins 2 .. 2047
+    assert p.algorithm() == "fft"
+    with pytest.raises(bridge.BridgeError):
+        p.set_algorithm("slide")
+    p.close()
