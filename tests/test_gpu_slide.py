@@ -295,3 +295,15 @@ def test_slide_topk_refusals(gpu_session):
     with pytest.raises(bridge.BridgeError):
         p.set_algorithm("slide")
     p.close()
+
+
+def test_slide_topk_host_batch_path(gpu_session):
+    """gpu_spectrum_topk_batch (host buffers, chunked per stream, per-part seed workspace) with hop = 1
+    takes the sliding top-k per chunk; the per-bar CPU reference is the oracle's scan."""
+    n, bars = 4096, 60000
+    s = synth.random_walk(bars, seed=41)
+    got = bridge.spectrum_topk_batch(s, n, 1, "mean", "hann", top_k=8)
+    want = oracle.batch_topk(s, n, 1, "mean", "hann", 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, "mean", "hann")
+    kmin, kmax = oracle.band(n)
+    _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
