@@ -2,6 +2,7 @@
 // the spectrum kernel (one instantiation per N, detrend, output, window class).
 #pragma once
 #include <cmath>
+#include <type_traits>
 
 #include "spectrum_core.h"
 
@@ -102,10 +103,11 @@ template <typename T, int LOG2N, int VAR> constexpr bool band_fits(int span) {
 
 // Non-temporal sample loads as a compile-time variant (kVarNtLoad) where the windows do not overlap:
 // the run-time form (a.nt) costs the north-star kernel 4 % (539-540 vs 518 us per launch on one box,
-// kbench store mode, profiles/r02/kbench_ns_ntload.log).  Instantiated for every output but packed at
-// N >= 1024 without the IIR detrend; elsewhere a.nt still selects the loads at run time.
+// kbench store mode, profiles/r02/kbench_ns_ntload.log).  Instantiated for the power and top-k outputs at
+// N >= 1024 without the IIR detrend (the phase outputs measured within noise of the run-time form and would
+// double the longest translation unit); elsewhere a.nt still selects the loads at run time.
 template <typename T, int LOG2N, int DETREND, int OUT, int VAR> constexpr bool ct_nt_variant() {
-    return !(VAR & kVarNtLoad) && OUT != kOutPacked && LOG2N >= 10 && DETREND != kDetrendIir;
+    return !(VAR & kVarNtLoad) && (OUT == kOutPower || OUT == kOutTopK) && LOG2N >= 10 && DETREND != kDetrendIir;
 }
 
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR = default_var<T, LOG2N, DETREND, OUT>()>
@@ -192,6 +194,30 @@ template <typename T, int OSET = kSetBase> hipError_t dispatch_n(const SpectrumL
     default: return hipErrorInvalidValue;
     }
 }
+
+// The log2 N in [LO, HI] part of dispatch_n: the library compiles its instantiations in several
+// translation units (spectrum_f64*.hip, spectrum_f32*.hip, spectrum_phase*.hip) so they build in parallel.
+template <typename T, int OSET, int LO, int HI> hipError_t dispatch_n_range(const SpectrumLaunch &L, hipStream_t s) {
+    if (L.n_windows <= 0) return hipSuccess;
+    hipError_t e = hipErrorInvalidValue;
+    auto one = [&](auto lg) {
+        constexpr int G = decltype(lg)::value;
+        if constexpr (G >= LO && G <= HI)
+            if (L.log2n == G) e = dispatch_detrend<T, G, OSET>(L, s);
+    };
+    one(std::integral_constant<int, 5>{});
+    one(std::integral_constant<int, 6>{});
+    one(std::integral_constant<int, 7>{});
+    one(std::integral_constant<int, 8>{});
+    one(std::integral_constant<int, 9>{});
+    one(std::integral_constant<int, 10>{});
+    one(std::integral_constant<int, 11>{});
+    one(std::integral_constant<int, 12>{});
+    one(std::integral_constant<int, 13>{});
+    one(std::integral_constant<int, 14>{});
+    return e;
+}
+constexpr int kSplitLog2N = 12;  // first log2 N of the second translation unit of each precision / output set
 
 }  // namespace core
 }  // namespace wsp

@@ -43,6 +43,10 @@ struct SpectrumLaunch {
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);
 hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t stream);
 hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t stream);  // kOutPhase, kOutTopKPhase (f64)
+// the same for log2 N >= 12, compiled in translation units of their own (spectrum_*_hi.hip)
+hipError_t launch_spectrum_f64_hi(const SpectrumLaunch &L, hipStream_t stream);
+hipError_t launch_spectrum_f32_hi(const SpectrumLaunch &L, hipStream_t stream);
+hipError_t launch_spectrum_phase_hi(const SpectrumLaunch &L, hipStream_t stream);
 
 // Inverse real FFT of packed spectra (gpu_fft_real_inverse,
 // L/WaveSpecZZ_1.0.4-core.mq5:65,426): n_windows rows of N doubles in the
