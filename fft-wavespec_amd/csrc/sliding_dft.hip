@@ -281,9 +281,12 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
 // ---- hop = 1 top-k records (MTB_OUT_TOPK): only the band's bins are tracked.
 // Seeds of every segment into the workspace: [NF][span] trackers of bins kmin .. kmin + span - 1, then
 // {sum of x - L (mean path), L}; one workgroup per segment, the same in-LDS FFTs as slide_kernel.
+// threads of the seed pass: N/4 (one radix-4 butterfly per thread and stage), at most 1024
+template <int LOG2N> constexpr int seed_nt() { return (1 << LOG2N) / 4 < 1024 ? (1 << LOG2N) / 4 : 1024; }
+
 template <typename T, int LOG2N, int NF, int DETREND>
-__global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>())) void slide_seed_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, NT = N / (2 * slide_b<LOG2N>());
+__global__ __launch_bounds__(seed_nt<LOG2N>()) void slide_seed_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, NT = seed_nt<LOG2N>();
     constexpr bool TWL = N <= 4096;
     __shared__ d2 lds[N];
     __shared__ d2 twq[TWL ? N / 4 : 1];
@@ -369,9 +372,9 @@ __global__ __launch_bounds__(64) void slide_topk_kernel(SlideArgs a) {
 }
 
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
-    constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
-    hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0, s,
+                       a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int nb = (a.span + 63) / 64;
