@@ -29,6 +29,10 @@
 // Rounding: a tracker's error grows at most linearly with the segment length (<= 256 steps by
 // default: ~3e-14 of its own magnitude); the parity bars are BASELINE.md 2's (tests/test_gpu_slide.py,
 // tests/test_gpu_fullgrid.py, the CPU model tests/test_slide_model.py).
+//
+// Top-k records (MTB_OUT_TOPK, fp64) at hop = 1 track only the scan band's bins: slide_seed_kernel writes every
+// segment's band trackers to the plan workspace, slide_topk_kernel slides them one wave per segment and runs the FFT
+// kernel's one-wave scan (core::topk_wave64) on each window's band, staged in LDS.
 #include <atomic>
 
 #include "spectrum_core.h"  // topk_wave64: the one-wave top-k scan of the FFT kernel
