@@ -463,9 +463,13 @@ def main(argv=None):
     total_windows = ctl.sum(float(wl.windows * args.steps))
     value = total_windows / secs
     baseline = baseline_all = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.cpu_cfg is not None:
-        baseline = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], args.cpu_seconds)
-        baseline_all = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], args.cpu_seconds / 2, cpu_threads())
+    # The CPU baseline beside every line (north star: "next to the reference CPU path timed on the GPU
+    # box's own host cores in the same run"), on rank 0 after the timed region, so it never overlaps the
+    # GPU timing; with N > 1 ranks the sample is halved to keep the driver's 1/2/4/8 sweep short.
+    if rank == 0 and not args.no_cpu_baseline and wl.cpu_cfg is not None:
+        budget = args.cpu_seconds if world == 1 else args.cpu_seconds / 2
+        baseline = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], budget)
+        baseline_all = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], budget / 2, cpu_threads())
 
     if rank == 0:
         line = {

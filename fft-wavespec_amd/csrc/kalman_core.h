@@ -16,10 +16,12 @@
 //  * the covariance is carried as the 10 entries of the symmetric P (the
 //    reference's 16-entry expansion is algebraically symmetric: each P_ij
 //    update equals P_ji's), ~40 % fewer operations per step;
-//  * the state is centred on the window's first sample (z' = z - x0, pos' =
-//    pos - x0): the filter is exactly shift-equivariant (innovation, gain,
-//    boost and clip depend only on differences), and centring lets the fp32
-//    plan run the filter in fp32 without cancelling against the price level.
+//  * the state is centred on the first sample b of the lane's current LDS tile
+//    (z' = z - b, pos' = pos - b, re-centred every J steps): the filter is
+//    exactly shift-equivariant (innovation, gain, boost and clip depend only on
+//    differences; only pos and the EMA carry the level), and centring lets the
+//    fp32 plan run the filter in fp32 without cancelling against the price
+//    level -- or against a level jump earlier in the window.
 // Output: d = x - trend rounded to the plan's element type, consumed by the
 // spectrum kernel as a hop = N series.
 #pragma once
@@ -72,7 +74,7 @@ inline int kalman_flags(const KP &kp) {
     return (kp.adapt > 0.0 ? kKfAdapt : 0) | (kp.clip > 0.0 ? kKfClip : 0) | (kp.ema > 0.0 ? kKfEma : 0);
 }
 
-// Filter state of one lane (centred on the window's first sample x0) and the
+// Filter state of one lane (centred on its tile's first sample) and the
 // step constants.
 template <typename K> struct KState {
     K pos, vel, acc, jerk;
@@ -106,7 +108,7 @@ template <typename K, int FL> __device__ __forceinline__ KConst<K> kconst(const 
     return c;
 }
 
-// ResetKalmanState(first_meas) :2015-2029, centred: pos = first_meas - x0
+// ResetKalmanState(first_meas) :2015-2029, centred: pos = first_meas - centre
 template <typename K> __device__ __forceinline__ void kreset(KState<K> &s, const KP &kp, K pos0) {
     s.pos = pos0;
     s.vel = (K)kp.iv;
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
     };
 
     KState<K> st;
-    T x0 = 0;
+    T base = 0, base_at_warm = 0;  // the lane's current centre: the first sample of its current tile
     const int lr = lane_on ? l : 0;
     // filters chunks [c0, c1) of every lane; stores the rows of segment 0 for c >= s0 and of segment 1
     // for c >= s1 (SEG = 2: its warm-up chunks produce no output)
@@ -354,22 +356,30 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
             for (int i = 0; i < NI; ++i) tile[(i * RPI + lrow) * (J + 1) + lcol] = reg[i];
             __syncthreads();
             if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
-            if (c == 0) {
-                x0 = tile[(SEG == 2 ? lr % 32 : lr) * (J + 1)];  // the window's first sample
-                const T first = tile[lr * (J + 1)];             // this lane's first sample
-                kreset<K>(st, kp, (K)(first - x0));
-            }
             T zrow[J];  // this row's J samples in registers: no LDS latency inside the recurrence
 #pragma unroll
             for (int j = 0; j < J; ++j) zrow[j] = tile[lr * (J + 1) + j];
+            // re-centre on the tile's first sample (shift-equivariance: only pos and the EMA carry the
+            // level); the shift base - zrow[0] is exact for prices within 2x of each other (Sterbenz)
+            if (c == 0) {
+                kreset<K>(st, kp, K(0));
+            } else {
+                const K sh = (K)(base - zrow[0]);
+                st.pos += sh;
+                st.ema_prev += sh;
+            }
+            base = zrow[0];
 #pragma unroll UNROLL
             for (int j = 0; j < J; ++j) {
-                const K z = (K)(zrow[j] - x0);  // exact for prices within 2x of x0 (Sterbenz)
+                const K z = (K)(zrow[j] - base);  // exact for prices within 2x of the tile's first (Sterbenz)
                 const K trend = kstep<K, TWO, PKUP>(st, kc, z);
                 zrow[j] = T(z - trend);
             }
             if constexpr (SEG == 2) {
-                if (save_warm && c == WUC - 1) warm = st;  // the second lanes' state after sample L0 - 1
+                if (save_warm && c == WUC - 1) {  // the second lanes' state after sample L0 - 1
+                    warm = st;
+                    base_at_warm = base;
+                }
             }
             if (lane_on) {
 #pragma unroll
@@ -414,12 +424,13 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
         }
         if (__ballot(!ok)) {  // wave-uniform: the second lanes re-run [L0, N) from the exact state
             if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
-            const T x0keep = x0;
             st = ex;
+            // the exact state is centred on sample L0 - J (the first lanes' last tile), which is the
+            // second lanes' own centre of tile WUC - 1
+            base = base_at_warm;
             // chunks WUC .. nchunks-1 of the second segment; the first lanes recompute their own last
             // chunks' values, which are not stored (s0 past the end)
             run(WUC, nchunks, nchunks, WUC, false, warm);
-            x0 = x0keep;
         }
     }
 }
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
 // after 256 steps in fp64, 1-6 ulps in fp32).  The warm-up is VERIFIED per window: after its
 // last step segment A holds the exact state at sample L0 - 1, which segment B reached after its
 // warm-up (kept from then); every component must agree within 2^-16 relative plus an absolute
-// floor of 2^-24 (|x0| + |pos|) -- half an fp32 ulp of the price level, below what an fp32
+// floor of 2^-24 (|centre| + |pos|) -- half an fp32 ulp of the price level, below what an fp32
 // series can resolve.  Any window that fails makes its wave re-run [L0, N) from segment A's
 // exact state (wave-uniform branch), so a filter that has not converged is never used.  The
 // outputs agree with the sequential fp32 filter to the fp32 rounding of the state (not bit for
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     auto tpos = [&](int g) { return (8 * g + rl) * RS + 4 * q; };  // pair index of an IO lane's first sample
 
     KState2 st;
-    float x0 = 0.f;
+    kf2 base = {0.f, 0.f};  // each segment's centre: the first sample of its current tile
     KState<float> warm;  // segment B's state after its warm-up
     auto stage = [&]() {  // the loaded rows of both segments -> (A, B) pairs in the tile
 #pragma unroll
@@ -607,16 +618,6 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 __syncthreads();
                 if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
             }
-            if (c == 0) {
-                const kf2 f = tile[l * RS];  // (sample 0, sample L0 - WU)
-                x0 = f.x;
-                KState<float> a;
-                kreset<float>(a, kp, 0.f);
-                st.pos = kf2{0.f, f.y - x0};
-                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
-                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
-                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
-            }
             kf2 zrow[J];
 #pragma unroll
             for (int j = 0; j < J; j += 2) {
@@ -624,9 +625,26 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 zrow[j] = kf2{v.x, v.y};
                 zrow[j + 1] = kf2{v.z, v.w};
             }
+            // Re-centre both segments on their tile's first sample.  StepKalman4D is exactly
+            // shift-equivariant (only pos carries the level: innovation, gain, boost and clip see
+            // differences), so moving the centre is exact up to one rounding of pos per tile, and
+            // pos stays at the size of the local excursion instead of the distance from sample 0:
+            // a 0.5 level jump inside a window then costs fp32 no precision (2e-5 -> 1e-6 of the
+            // spectrum, scripts/kalman_f32_emulation.py).  base - zrow[0] is exact (Sterbenz).
+            if (c == 0) {  // (sample 0, sample L0 - WU): both segments reset at their first sample
+                KState<float> a;
+                kreset<float>(a, kp, 0.f);
+                st.pos = kf2{0.f, 0.f};
+                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
+                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
+                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
+            } else {
+                st.pos += base - zrow[0];
+            }
+            base = zrow[0];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
-                const kf2 z = zrow[j] - x0;  // exact for prices within 2x of x0 (Sterbenz)
+                const kf2 z = zrow[j] - base;  // exact for prices within 2x of the tile's first (Sterbenz)
                 const kf2 trend = kstep_pk2(st, kc, z);
                 zrow[j] = z - trend;
             }
@@ -659,8 +677,9 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         }
     };
     run(0, nchunks, 0, WUC, std::true_type{});
-    // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it
-    const float fl = 0x1p-24f * (fabsf(x0) + fabsf(st.pos.x));
+    // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it.
+    // Both are centred on sample L0 - J: segment A's last tile is segment B's tile WUC - 1.
+    const float fl = 0x1p-24f * (fabsf(base.x) + fabsf(st.pos.x));
     const bool ok = kagree(st.pos.x, warm.pos, fl) && kagree(st.vel.x, warm.vel, fl) && kagree(st.acc.x, warm.acc, fl) &&
                     kagree(st.jerk.x, warm.jerk, fl) && kagree(st.p00.x, warm.p00, 0.f) && kagree(st.p01.x, warm.p01, 0.f) &&
                     kagree(st.p02.x, warm.p02, 0.f) && kagree(st.p03.x, warm.p03, 0.f) && kagree(st.p11.x, warm.p11, 0.f) &&
@@ -672,6 +691,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         st.p00.y = st.p00.x, st.p01.y = st.p01.x, st.p02.y = st.p02.x, st.p03.y = st.p03.x;
         st.p11.y = st.p11.x, st.p12.y = st.p12.x, st.p13.y = st.p13.x, st.p22.y = st.p22.x;
         st.p23.y = st.p23.x, st.p33.y = st.p33.x;
+        base.y = base.x;
         run(WUC, nchunks, nchunks, WUC, std::false_type{});  // only segment B stores
     }
 }
@@ -707,9 +727,9 @@ __device__ __forceinline__ void kset(KState2 &s, int h, const KState<float> &r) 
     p(s.p12, r.p12), p(s.p13, r.p13), p(s.p22, r.p22), p(s.p23, r.p23), p(s.p33, r.p33);
 }
 // the warm-up check of kalman_pk2_kernel: every component within 2^-16 relative, the state
-// additionally within 2^-24 (|x0| + |pos|) absolute
-__device__ __forceinline__ bool kagree_state(const KState<float> &e, const KState<float> &w, float x0) {
-    const float fl = 0x1p-24f * (fabsf(x0) + fabsf(e.pos));
+// additionally within 2^-24 (|centre| + |pos|) absolute
+__device__ __forceinline__ bool kagree_state(const KState<float> &e, const KState<float> &w, float centre) {
+    const float fl = 0x1p-24f * (fabsf(centre) + fabsf(e.pos));
     return kagree(e.pos, w.pos, fl) && kagree(e.vel, w.vel, fl) && kagree(e.acc, w.acc, fl) && kagree(e.jerk, w.jerk, fl) &&
            kagree(e.p00, w.p00, 0.f) && kagree(e.p01, w.p01, 0.f) && kagree(e.p02, w.p02, 0.f) && kagree(e.p03, w.p03, 0.f) &&
            kagree(e.p11, w.p11, 0.f) && kagree(e.p12, w.p12, 0.f) && kagree(e.p13, w.p13, 0.f) && kagree(e.p22, w.p22, 0.f) &&
@@ -774,7 +794,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void ka
     auto tpos = [&](int g) { return (RPI * g + rl) * RS + 4 * q; };
 
     KState2 st, warm2;
-    float x0 = 0.f;
+    kf2 base = {0.f, 0.f}, wbase = {0.f, 0.f};  // segment centres (first sample of the current tile), at WUC - 1
     // sm: segments whose rows this pass stores (segment k from chunk 0 if k == 0, else from WUC)
     auto run = [&](int c0, int c1, unsigned sm) {
         issue(c0);
@@ -787,17 +807,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void ka
             }
             __syncthreads();
             if (c + 1 < c1) issue(c + 1);
-            if (c == 0) {
-                const kf2 f = tile[l * RS];  // first samples of this lane's two segments
-                const float t = kxor32(f.x);
-                x0 = hi ? t : f.x;  // window's sample 0, from lane l - 32 for the upper lanes
-                KState<float> a;
-                kreset<float>(a, kp, 0.f);
-                st.pos = f - x0;
-                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
-                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
-                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
-            }
             kf2 zrow[J];
 #pragma unroll
             for (int j = 0; j < J; j += 2) {
@@ -805,13 +814,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void ka
                 zrow[j] = kf2{v.x, v.y};
                 zrow[j + 1] = kf2{v.z, v.w};
             }
+            if (c == 0) {  // every segment resets at its first sample; re-centred per tile (kalman_pk2_kernel)
+                KState<float> a;
+                kreset<float>(a, kp, 0.f);
+                st.pos = kf2{0.f, 0.f};
+                st.vel = kf2{a.vel, a.vel}, st.acc = kf2{a.acc, a.acc}, st.jerk = kf2{a.jerk, a.jerk};
+                st.p00 = kf2{a.p00, a.p00}, st.p11 = kf2{a.p11, a.p11}, st.p22 = kf2{a.p22, a.p22}, st.p33 = kf2{a.p33, a.p33};
+                st.p01 = st.p02 = st.p03 = st.p12 = st.p13 = st.p23 = kf2{0.f, 0.f};
+            } else {
+                st.pos += base - zrow[0];
+            }
+            base = zrow[0];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
-                const kf2 z = zrow[j] - x0;
+                const kf2 z = zrow[j] - base;
                 const kf2 trend = kstep_pk2(st, kc, z);
                 zrow[j] = z - trend;
             }
-            if (c == WUC - 1) warm2 = st;
+            if (c == WUC - 1) {
+                warm2 = st;
+                wbase = base;
+            }
 #pragma unroll
             for (int j = 0; j < J; j += 2)
                 *reinterpret_cast<f4v *>(tile + l * RS + j) = f4v{zrow[j].x, zrow[j].y, zrow[j + 1].x, zrow[j + 1].y};
@@ -832,25 +855,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void ka
     const KState2 fin = st;
     // 0 -> 1 (lanes < 32): segment 1's warm-up against segment 0's exact final state
     KState<float> s1 = kget(fin, 1);
-    if (__ballot(!hi && !kagree_state(kget(fin, 0), kget(warm2, 1), x0))) {
+    // (a predecessor's last tile is its successor's tile WUC - 1: both states sit on the successor's wbase)
+    if (__ballot(!hi && !kagree_state(kget(fin, 0), kget(warm2, 1), wbase.y))) {
         if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
         kset(st, 1, kget(fin, 0));
+        base.y = wbase.y;
         run(WUC, nchunks, 0x2u);
         s1 = kget(st, 1);
     }
     // 1 -> 2 (across the pair): segment 2's warm-up (lane l + 32) against segment 1's final (lane l)
     s1 = kxor32_state(s1);
     KState<float> s2 = kget(fin, 0);
-    if (__ballot(hi && !kagree_state(s1, kget(warm2, 0), x0))) {
+    if (__ballot(hi && !kagree_state(s1, kget(warm2, 0), wbase.x))) {
         if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
         kset(st, 0, s1);
+        base.x = wbase.x;
         run(WUC, nchunks, 0x4u);
         s2 = kget(st, 0);
     }
     // 2 -> 3 (lanes >= 32)
-    if (__ballot(hi && !kagree_state(s2, kget(warm2, 1), x0))) {
+    if (__ballot(hi && !kagree_state(s2, kget(warm2, 1), wbase.y))) {
         if (fallbacks && l == 0) atomicAdd(fallbacks, 1u);
         kset(st, 1, s2);
+        base.y = wbase.y;
         run(WUC, nchunks, 0x8u);
     }
 }

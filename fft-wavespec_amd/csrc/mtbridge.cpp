@@ -934,6 +934,12 @@ void release_jobs(bool all, std::thread::id owner) {
 // The workspace is a shared_ptr: an execute holds the one it enqueued with, so a reconfiguration that
 // needs a larger one (wsp_plan_set_topk / _set_algorithm / _set_slide_segment) swaps it without freeing
 // memory a queued launch still uses (the last holder frees it after the device has finished).
+//
+// A plan with a workspace (Kalman / IIR pre-pass windows, large-N column results, hop = 1 top-k
+// segment seeds) is stateful on the device: two executes may not overlap.  wsp_plan_execute orders
+// them itself -- each records `done` on its stream, and an execute on a different stream first waits
+// for it (hipStreamWaitEvent: device-side ordering, no host sync) -- so one plan may be driven from
+// several streams and threads.  Plans without a workspace run concurrently.
 struct Plan {
     int dev = 0;
     std::mutex mu;
@@ -941,18 +947,44 @@ struct Plan {
     double kalman[16];
     std::shared_ptr<void> ws;
     size_t ws_bytes = 0;
+    hipEvent_t done = nullptr;       // the last workspace execute's completion
+    hipStream_t done_stream = nullptr;
+    bool done_recorded = false;
+    ~Plan() {
+        if (done) (void)hipEventDestroy(done);
+    }
 };
+
+// Retired plan workspaces.  Dropping the last reference to a workspace can happen at the end of a
+// wsp_plan_execute (a reconfiguration or wsp_plan_destroy raced with it), and hipFree would wait for
+// the whole device there -- every other chart's stream included.  So the deleter only parks the
+// block; the configuration calls (plan create / set / destroy, gpu_shutdown), which may block, free
+// the parked blocks after a device sync.
+std::mutex g_ws_grave_mu;
+std::vector<std::pair<int, void *>> *g_ws_grave = new std::vector<std::pair<int, void *>>();
+void ws_reap() {
+    std::vector<std::pair<int, void *>> v;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_grave_mu);
+        v.swap(*g_ws_grave);
+    }
+    for (auto &e : v) {
+        (void)hipSetDevice(e.first);
+        (void)hipDeviceSynchronize();  // queued launches may still read it
+        (void)hipFree(e.second);
+    }
+}
 std::shared_ptr<void> plan_ws_alloc(int dev, size_t bytes) {
     void *d = nullptr;
     if (hipSetDevice(dev) != hipSuccess || hipMalloc(&d, bytes) != hipSuccess) return nullptr;
     return std::shared_ptr<void>(d, [dev](void *q) {
-        (void)hipSetDevice(dev);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(q);
+        std::lock_guard<std::mutex> lk(g_ws_grave_mu);
+        g_ws_grave->emplace_back(dev, q);
     });
 }
 // (under p->mu) grow the workspace to what cfg needs
 int plan_ws_fit(Plan &p) {
+    ws_reap();
     const size_t need = ws_layout(p.cfg).total;
     if (need <= p.ws_bytes) return MTB_OK;
     auto w = plan_ws_alloc(p.dev, need);
@@ -1096,6 +1128,7 @@ MTB_API void gpu_shutdown(void) {
         release_jobs(true, me);  // ~Batch waits for in-flight work
         S.reset();               // streams go with the last holder (calls in flight keep their own reference)
         pool_release_all();
+        ws_reap();
     } else if (mine) {
         release_jobs(false, me);
     }
@@ -1381,7 +1414,10 @@ MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t 
         return MTB_BAD_ARGS;
     }
     const int st = batch_poll(*b, false);
-    if (st == MTB_NOT_READY) return MTB_NOT_READY;
+    // pending: MTB_OK + ready = 0.  WaveCyclesBatchFetcher.mq5:127-131 sleeps only on OK with
+    // ready == 0 and re-polls at once on NOT_READY (4000 tries spent in microseconds); the
+    // indicator's warm-up loop (1.1.0:1029-1039) accepts both conventions.
+    if (st == MTB_NOT_READY) return MTB_OK;
     if (ready) *ready = 1;
     if (st != MTB_OK) return st;
     if (!out || out_cap < b->cfg.record()) {
@@ -1525,14 +1561,31 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
         set_error("wsp_plan_execute: null device buffer");
         return MTB_BAD_ARGS;
     }
+    const hipStream_t stream = (hipStream_t)hip_stream;
     Config c;
     std::shared_ptr<void> ws;
     {
         std::lock_guard<std::mutex> lk(p->mu);
         c = p->cfg;
         ws = p->ws;
+        if (ws) {  // stateful on the device: ordered after the previous execute (struct Plan)
+            if (!p->done) {
+                if (hipSetDevice(p->dev) != hipSuccess || hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess) {
+                    p->done = nullptr;
+                    set_error("wsp_plan_execute: cannot create the plan's event");
+                    return MTB_INTERNAL_ERROR;
+                }
+            }
+            if (p->done_recorded && p->done_stream != stream) HIP_OR(hipStreamWaitEvent(stream, p->done, 0), MTB_INTERNAL_ERROR);
+            const int st = enqueue(p->dev, c, p->kalman, d_series, d_out, ws.get(), stream);
+            if (st != MTB_OK) return st;
+            HIP_OR(hipEventRecord(p->done, stream), MTB_INTERNAL_ERROR);
+            p->done_recorded = true;
+            p->done_stream = stream;
+            return MTB_OK;
+        }
     }
-    return enqueue(p->dev, c, p->kalman, d_series, d_out, ws.get(), (hipStream_t)hip_stream);
+    return enqueue(p->dev, c, p->kalman, d_series, d_out, nullptr, stream);
 }
 
 MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period, double max_period) {
@@ -1581,11 +1634,16 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
     return sw;
 }
 
+// Longest sliding-DFT segment a caller may ask for: a tracker's rounding grows linearly with the
+// number of slides (sliding_dft.hip), and parity is tested up to this length
+// (tests/test_gpu_slide.py::test_slide_vs_fft_large_segments).
+constexpr int64_t kSlideMaxSegment = 2048;
+
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    if (!p || windows < 0) {
-        set_error("wsp_plan_set_slide_segment(%lld, %lld): unknown plan or negative length", (long long)plan,
-                  (long long)windows);
+    if (!p || windows < 0 || windows > kSlideMaxSegment) {
+        set_error("wsp_plan_set_slide_segment(%lld, %lld): unknown plan or length outside 0..%lld", (long long)plan,
+                  (long long)windows, (long long)kSlideMaxSegment);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);
@@ -1623,7 +1681,9 @@ MTB_API int32_t wsp_plan_destroy(int64_t plan) {
         p = std::move(it->second);
         g_plans->erase(it);
     }
-    return MTB_OK;  // the last reference (here, or an execute in flight) frees the workspace
+    p.reset();  // the last reference (here, or an execute in flight) retires the workspace
+    ws_reap();
+    return MTB_OK;
 }
 
 }  // extern "C"

@@ -3,7 +3,7 @@
 // it with the reference's own call sequences:
 //
 //   live   -- the per-bar OnCalculate loop of WaveSpecZZ_1.1.0-gpuopt.mq5:
-//             EnsureFeedCache (Include/FeedCache.mqh:84-163) -> per bar
+//             EnsureFeedCache (Include/FeedCache.mqh:36-115) -> per bar
 //             FeedBuilder::Build / BuildPlaPriceSeries (1.1.0:760-771) ->
 //             EnsureGpu (1.1.0:722-757) -> FftProcessor::Run (1.1.0:518-531:
 //             gpu_fft_real_forward + unpack + |X|^2).
@@ -13,7 +13,7 @@
 //
 // Usage: oncalculate_harness <libmtbridge.so> <mode live|batch> <feed.bin>
 //                            <N> <bars> <out.bin> [detrend window period prec]
-// feed.bin is the FeedCache file format (FeedCache.mqh:96-104, 150-157):
+// feed.bin is the FeedCache file format (FeedCache.mqh:49-67, 102-111):
 // int32 count, then `count` doubles, newest first (series order).
 // out.bin receives `bars` spectra of N/2 doubles, oldest window first.
 #include <dlfcn.h>
@@ -66,13 +66,13 @@ struct Bridge {
     }
 };
 
-// struct FeedCache (Include/FeedCache.mqh:68-75); close[] is newest first.
+// struct FeedCache (Include/FeedCache.mqh:20-27); close[] is newest first (:12, :69).
 struct FeedCache {
     std::vector<double> close;
     bool loaded = false;
 };
 
-bool load_feed_cache(const char *file, FeedCache &c) {  // FeedCache.mqh:93-109
+bool load_feed_cache(const char *file, FeedCache &c) {  // FeedCache.mqh:49-67
     FILE *f = fopen(file, "rb");
     if (!f) return false;
     int32_t cnt = 0;
@@ -166,11 +166,12 @@ int main(int argc, char **argv) {
         }
         int ready = 0, out_len = 0;
         const int cap = bars * (N / 2);
-        for (int polls = 0; polls < 4000; ++polls) {  // WaveCyclesBatchFetcher.mq5:127-131
+        // WaveCyclesBatchFetcher.mq5:126-132, unchanged: 4000 tries, Sleep(5) only on OK with ready == 0,
+        // break on any status other than OK / NOT_READY (a NOT_READY re-polls at once)
+        for (int tries = 0; tries < 4000 && ready == 0; ++tries) {
             st = br.try_get(jid, spectra.data(), cap, &out_len, &ready);
-            if (st == MTB_OK && ready == 1) break;
-            if (st != MTB_OK && st != MTB_NOT_READY) break;
-            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+            if (st == MTB_OK && ready == 0) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+            else if (st != MTB_OK && st != MTB_NOT_READY) break;
         }
         br.free_job(jid);
         if (st != MTB_OK || ready != 1 || out_len != bars) {

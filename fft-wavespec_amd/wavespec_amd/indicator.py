@@ -3,7 +3,7 @@
 Same names, argument meaning and error behaviour as the MQL5 code that calls
 ``mt-bridge.dll``; the arithmetic happens in libmtbridge.so (HIP, gfx950).
 
-* :class:`FeedCache` / :func:`ensure_feed_cache` -- Include/FeedCache.mqh:68-163
+* :class:`FeedCache` / :func:`ensure_feed_cache` -- Include/FeedCache.mqh:20-115
   (file format: int32 count + doubles, newest first); :func:`pin_feed_cache`
   keeps the history page-locked (gpu_register_host) so the batch path DMAs it
   in place -- the north star's "FeedCache rewired to pinned buffers".
@@ -31,13 +31,13 @@ ALGLIB_STATUS_NOT_READY = -5  # 1.1.0:16
 
 
 def feed_cache_file_name(prefix: str, symbol: str, tf: str) -> str:
-    """FeedCacheFileName, Include/FeedCache.mqh:78-81."""
+    """FeedCacheFileName, Include/FeedCache.mqh:30-33."""
     return f"{prefix}_cache_{symbol}_{tf}.bin"
 
 
 @dataclass
 class FeedCache:
-    """struct FeedCache, Include/FeedCache.mqh:68-75 (close[] newest first).
+    """struct FeedCache, Include/FeedCache.mqh:20-27 (close[] newest first, :12, :69).
 
     ``chrono`` is the same history oldest first in one contiguous float64 buffer: the physical
     memory of the MQL as-series close[] array, which is what the terminal hands the DLL.  Once
@@ -53,7 +53,7 @@ class FeedCache:
 
 
 def save_feed_cache(path: str, close_newest_first: np.ndarray) -> None:
-    """FileWriteInteger(count) + FileWriteArray(close) (FeedCache.mqh:150-157)."""
+    """FileWriteInteger(count) + FileWriteArray(close) (FeedCache.mqh:102-111)."""
     a = np.ascontiguousarray(close_newest_first, dtype="<f8")
     with open(path, "wb") as f:
         f.write(struct.pack("<i", a.size))
@@ -61,7 +61,7 @@ def save_feed_cache(path: str, close_newest_first: np.ndarray) -> None:
 
 
 def load_feed_cache(path: str) -> np.ndarray | None:
-    """FileReadInteger + FileReadArray (FeedCache.mqh:93-109)."""
+    """FileReadInteger + FileReadArray (FeedCache.mqh:49-67)."""
     if not os.path.exists(path):
         return None
     with open(path, "rb") as f:
@@ -76,7 +76,7 @@ def load_feed_cache(path: str) -> np.ndarray | None:
 
 def ensure_feed_cache(cache: FeedCache, symbol: str, tf: str, needed_bars: int, enable_cache: bool, prefix: str,
                       copy_close, cache_dir: str = ".") -> tuple[bool, int, bool]:
-    """EnsureFeedCache (FeedCache.mqh:84-163).
+    """EnsureFeedCache (FeedCache.mqh:36-115).
 
     ``copy_close(start, count)`` plays CopyClose(symbol, tf, start, count): it
     returns up to ``count`` closes newest-first starting ``start`` bars back.
@@ -92,7 +92,7 @@ def ensure_feed_cache(cache: FeedCache, symbol: str, tf: str, needed_bars: int, 
     if not (cache.symbol == symbol and cache.tf == tf):
         cache.close = np.empty(0)
     cached = cache.close.size
-    max_chunk = 100000  # :113
+    max_chunk = 100000  # :80
     parts = [cache.close]
     while cached < needed_bars:
         want = min(max_chunk, needed_bars - cached)
@@ -120,7 +120,11 @@ def _restage(cache: FeedCache) -> None:
         unpin_feed_cache(cache)
     cache.chrono = np.ascontiguousarray(cache.close[::-1], dtype=np.float64)
     if was:
-        pin_feed_cache(cache)
+        try:
+            pin_feed_cache(cache)
+        except bridge.BridgeError as e:  # the session is gone (last gpu_shutdown): stay unpinned
+            if e.status != bridge.BACKEND_UNAVAILABLE:
+                raise
 
 
 def pin_feed_cache(cache: FeedCache) -> None:
@@ -135,9 +139,17 @@ def pin_feed_cache(cache: FeedCache) -> None:
 
 
 def unpin_feed_cache(cache: FeedCache) -> None:
+    """gpu_unregister_host of the pinned history.  A registration belongs to the session: once the
+    last gpu_shutdown has torn the session down (FftProcessor.shutdown in on_calculate may be that
+    call) the library no longer holds it -- the pages were unlocked with the session -- so an
+    unknown buffer or a missing session leaves nothing to undo and only clears the flag."""
     if cache.pinned:
         cache.pinned = False
-        bridge.unregister_host(cache.chrono)
+        try:
+            bridge.unregister_host(cache.chrono)
+        except bridge.BridgeError as e:
+            if e.status not in (bridge.BAD_ARGS, bridge.BACKEND_UNAVAILABLE):
+                raise
 
 
 class FeedBuilder:

@@ -76,14 +76,24 @@ extern "C" {
  * 1. Reference surface -- Include/imports.mqh:5-19 (exact signatures)
  * ===================================================================== */
 
-/* imports.mqh:5.  Opens a session on `device_index` (0-based HIP device;
- * -1 = every visible GPU, windows of batch calls are sharded across them).
- * `stream_count` HIP streams per device (caller clamps 16..512, 1.1.0:729).
- * Idempotent; the caller retries it every bar until it succeeds
- * (1.1.0:722-751).  Returns MTB_OK or MTB_BACKEND_UNAVAILABLE. */
+/* imports.mqh:5.  Opens (first call) or joins the process-wide session on
+ * `device_index` (0-based HIP device; -1 = every visible GPU, windows of
+ * batch calls are sharded across them).  `stream_count` HIP streams per
+ * device (caller clamps 16..512, 1.1.0:729).  Every successful call adds one
+ * reference to the session and one to the calling thread's count (MT5 runs
+ * each chart on its own thread and each chart calls gpu_init once, EnsureGpu
+ * 1.1.0:722-751; a chart retries it every bar until it succeeds).  Returns
+ * MTB_OK, MTB_BACKEND_UNAVAILABLE (no usable device), or MTB_BAD_ARGS when a
+ * session is already open on a different device (it is not replaced). */
 MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count);
 
-/* imports.mqh:6.  Frees every job, stream and buffer (OnDeinit 1.1.0:706-716). */
+/* imports.mqh:6 (OnDeinit 1.1.0:706-716).  Drops one reference taken by
+ * gpu_init.  When the calling thread's own count reaches zero, the jobs that
+ * thread submitted are released (other charts' jobs are untouched); when the
+ * session's count reaches zero, every remaining job is released and the
+ * streams, pooled buffers and host registrations are freed once calls still
+ * in flight on other threads have returned.  Without an open session it is a
+ * no-op. */
 MTB_API void gpu_shutdown(void);
 
 /* imports.mqh:7; caller FftProcessor::Run 1.1.0:518-531.  Real forward DFT
@@ -182,8 +192,16 @@ MTB_API int32_t gpu_submit_spectrum_batch(const double *series, int32_t series_l
                                           int32_t hop, int32_t detrend, int32_t window, int32_t trend_period,
                                           int32_t precision, int32_t output, int64_t *job_id);
 
-/* Poll: MTB_NOT_READY + *ready=0 while pending; MTB_OK + *ready=1 when the
- * records are copied to out (1.1.0:1032-1035).  Caller frees the job. */
+/* Poll: MTB_OK + *ready=0 while pending; MTB_OK + *ready=1 when the records
+ * are copied to out.  The pending status is the one WaveCyclesBatchFetcher's
+ * unchanged loop needs (WaveCyclesBatchFetcher.mq5:127-131 sleeps only on
+ * OK && ready == 0 and re-polls at once on any other status, so a NOT_READY
+ * convention would spend its 4000 tries in microseconds); the indicator's
+ * warm-up loop (1.1.0:1029-1039) accepts it as well.  Any other status is an
+ * error (unknown job, device error, out_cap below one record).  The caller
+ * frees the job.  (The reference's single-job cycles poll, 1.1.0:1274, uses
+ * NOT_READY; the cycle functions are out of scope here and return
+ * MTB_BACKEND_UNAVAILABLE.) */
 MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t out_cap, int32_t *out_len,
                                            int32_t *ready);
 
@@ -211,7 +229,7 @@ MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
 
 /* Pinned feed staging (north star: "FeedCache.mqh rewired to stage price bars
  * into pinned host buffers for hipMemcpyAsync").  Replaces the FeedCache
- * close-history array's plain host memory (Include/FeedCache.mqh:84-114,
+ * close-history array's plain host memory (Include/FeedCache.mqh:36-115,
  * `struct FeedCache`) as the staging area: the caller page-locks the array it
  * already keeps (hipHostRegister, portable across the session's devices) after
  * each ArrayResize, and the synchronous batch calls (gpu_spectrum_batch, the
@@ -248,7 +266,15 @@ MTB_API int64_t wsp_plan_create_inverse(int32_t device, int32_t window_len, int6
 /* Enqueues the hot path on `hip_stream` (a hipStream_t; NULL = the null
  * stream) reading d_series (device pointer, double or float per the plan's
  * precision, >= (n_windows-1)*hop + window_len elements) and writing d_out
- * (n_windows * record elements).  Asynchronous; no allocation, no sync. */
+ * (n_windows * record elements).  Asynchronous; no allocation, no host
+ * sync.  A plan with a device workspace (Kalman detrend, IIR above 16384,
+ * window_len above 16384, hop = 1 top-k by the sliding DFT) orders its own
+ * executes: one issued on a different stream than the previous execute waits
+ * for it on the device (hipStreamWaitEvent), so such a plan may be executed
+ * from several streams and threads but its executes never overlap; plans
+ * without a workspace run concurrently on any number of streams.  A
+ * workspace replaced by a reconfiguration is freed by the next configuration
+ * call (create / set / destroy / gpu_shutdown), never inside an execute. */
 MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out, void *hip_stream);
 
 /* Sets a top-k plan's scan: MTB_OUT_TOPK (4*top_k elements per window; a
@@ -268,7 +294,9 @@ MTB_API int32_t wsp_plan_set_topk(int64_t plan, int32_t top_k, double min_period
 #define MTB_ALGO_SLIDE 2
 MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
 /* Tuning: windows per sliding-DFT workgroup (each seeds its trackers once);
- * 0 = the library's policy.  MTB_BAD_ARGS for an unknown plan or windows < 0. */
+ * 0 = the library's policy (32..256).  A tracker's rounding grows with the
+ * number of slides, so at most 2048 (the longest length the parity tests
+ * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);

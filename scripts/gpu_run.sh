@@ -1,0 +1,103 @@
+#!/bin/bash
+# The one GPU-box runner: executes the given steps in order, each under its own time limit, and stops
+# at the first step that fails (a fault, abort, time limit or test failure ends the call there).
+# Everything lands under gpurun_out/<tag>/; copy what is to be judged into profiles/.
+#
+#   gpurun -- bash scripts/gpu_run.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   tests[=<pytest args>]    pytest -m gpu (default: the whole GPU suite; args comma-separated, '+' = space
+#                            inside one, e.g. tests=tests/test_gpu_parity.py,-k,kalman+or+jump), log tests.log
+#   smoke                    __graft_entry__.smoke()
+#   bench=<cfg>[,<args>]     python bench.py --config <cfg> --steps 100 --warmup 20 --no-cpu-baseline <args>
+#                            (args comma-separated), line bench_<cfg>.json
+#   default                  python bench.py (the driver's default line, CPU baseline included)
+#   prof=<cfg>[,<algo>]      rocprofv3 kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own
+#                            passes (scripts/gpu_profile.sh), parsed by scripts/parse_prof.py
+#   sq=<cfg>,<counters>      one rocprofv3 --pmc pass with the given SQ_ counters (<= 8), sq_<cfg>.csv
+#   kbench=<args>            fft-wavespec_amd/bin/kbench <args> (spaces as commas)
+#   kalman=<args>            fft-wavespec_amd/bin/kalman_bench <args>
+#   harness=<args>           python scripts/<args> (a host-path timing script), spaces as commas
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+run() {  # run <seconds> <stdout file> <stderr file> <cmd...>
+    local t=$1 out=$2 err=$3
+    shift 3
+    if [ "$out" = "$err" ]; then
+        timeout -k 10 "$t" "$@" > "$out" 2>&1
+    else
+        timeout -k 10 "$t" "$@" > "$out" 2> "$err"
+    fi
+    local rc=$?
+    echo "[$TAG] rc=$rc: $*"
+    if [ $rc -ne 0 ]; then
+        tail -40 "$out"
+        tail -20 "$err"
+        exit $rc
+    fi
+}
+for step in "$@"; do
+    key=${step%%=*}
+    val=""
+    [ "$key" != "$step" ] && val=${step#*=}
+    case $key in
+    tests)
+        # comma-separated pytest arguments; '+' stands for a space inside one argument (-k expressions)
+        IFS=',' read -ra targs <<< "${val:-tests}"
+        for i in "${!targs[@]}"; do targs[$i]=${targs[$i]//+/ }; done
+        run 1100 $O/tests.log $O/tests.log python -u -m pytest "${targs[@]}" -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread
+        tail -3 $O/tests.log
+        ;;
+    smoke)
+        run 120 $O/smoke.log $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+        cat $O/smoke.log
+        ;;
+    bench)
+        cfg=${val%%,*}
+        extra=""
+        [ "$cfg" != "$val" ] && extra=${val#*,}
+        run 300 $O/bench_$cfg.json $O/bench_$cfg.err python bench.py --config $cfg --steps 100 --warmup 20 --no-cpu-baseline ${extra//,/ }
+        python3 -c "
+import json; d=json.loads(open('$O/bench_$cfg.json').read().strip().splitlines()[-1])
+print('$cfg', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g win/s'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+        ;;
+    default)
+        run 400 $O/bench_default.json $O/bench_default.err python bench.py
+        cat $O/bench_default.json
+        ;;
+    prof)
+        cfg=${val%%,*}
+        algo=auto
+        [ "$cfg" != "$val" ] && algo=${val#*,}
+        run 900 $O/prof_$cfg.log $O/prof_$cfg.log bash scripts/gpu_profile.sh $TAG $cfg $algo
+        cat $O/prof_$cfg.log
+        ;;
+    sq)
+        cfg=${val%%,*}
+        ctr=${val#*,}
+        run 120 $O/sq_$cfg.log $O/sq_$cfg.log rocprofv3 --pmc ${ctr//,/ } --kernel-trace --output-format csv -d $O/sq_$cfg -o run -- \
+            python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline
+        ;;
+    kbench)
+        run 300 $O/kbench.log $O/kbench.log fft-wavespec_amd/bin/kbench ${val//,/ }
+        cat $O/kbench.log
+        ;;
+    kalman)
+        run 300 $O/kalman_bench.log $O/kalman_bench.log fft-wavespec_amd/bin/kalman_bench ${val//,/ }
+        cat $O/kalman_bench.log
+        ;;
+    harness)
+        run 300 $O/harness_${val%%,*}.log $O/harness_${val%%,*}.log python3 scripts/${val//,/ }
+        cat $O/harness_${val%%,*}.log
+        ;;
+    *)
+        echo "unknown step $step"
+        exit 2
+        ;;
+    esac
+done

@@ -12,6 +12,14 @@
 // The launch stubs write a deterministic function of each window's own input
 // samples, so a driver can check that every record was routed to the right
 // place: record element k of window w = series[w*hop + k % N] + k.
+//
+// Devices: WSP_FAKE_DEVICES (default 1).  Streams, events and hipMalloc'd
+// blocks remember the device current at their creation; every copy and launch
+// checks that its stream and every device buffer it touches belong to the
+// device current on the calling thread (a part of a multi-GPU batch enqueued on
+// another device's stream or buffer counts as a violation), and launches count
+// the windows each device computed (fakehip_windows / fakehip_violations,
+// driven by multidev.cpp).
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
@@ -20,12 +28,15 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <initializer_list>
+#include <map>
 #include <mutex>
 #include <thread>
 
 #include "../../fft-wavespec_amd/csrc/wsp_internal.h"
 
 struct ihipStream_t {
+    int dev = 0;
     std::mutex mu;
     std::condition_variable cv, idle;
     std::deque<std::function<void()>> q;
@@ -88,6 +99,31 @@ void run_on(hipStream_t s, std::function<void()> f) {
     if (s) s->push(std::move(f));
     else f();
 }
+// device memory: base -> (bytes, device)
+std::mutex g_alloc_mu;
+std::map<uintptr_t, std::pair<size_t, int>> g_allocs;
+int dev_of(const void *p) {  // -1: not device memory (host, pinned or registered)
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    auto it = g_allocs.upper_bound(a);
+    if (it == g_allocs.begin()) return -1;
+    --it;
+    return a < it->first + it->second.first ? it->second.second : -1;
+}
+constexpr int kMaxDev = 64;
+std::atomic<int64_t> g_windows[kMaxDev];
+std::atomic<int64_t> g_violations{0};
+// an operation enqueued on stream s touching the given buffers, on the thread's current device
+void check_op(hipStream_t s, std::initializer_list<const void *> bufs, int64_t windows = 0) {
+    const int d = t_device;
+    bool bad = s && s->dev != d;
+    for (const void *b : bufs) {
+        const int bd = b ? dev_of(b) : -1;
+        if (bd >= 0 && bd != d) bad = true;
+    }
+    if (bad) g_violations++;
+    if (d >= 0 && d < kMaxDev) g_windows[d] += windows;
+}
 }  // namespace
 
 extern "C" {
@@ -102,14 +138,27 @@ hipError_t hipSetDevice(int d) {
 }
 hipError_t hipMalloc(void **p, size_t n) {
     *p = aligned_alloc(256, (n + 255) & ~size_t(255));
-    return *p ? hipSuccess : hipErrorOutOfMemory;
+    if (!*p) return hipErrorOutOfMemory;
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_allocs[(uintptr_t)*p] = {n ? n : 1, t_device};
+    return hipSuccess;
 }
 hipError_t hipFree(void *p) {
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        g_allocs.erase((uintptr_t)p);
+    }
     free(p);
     return hipSuccess;
 }
-hipError_t hipHostMalloc(void **p, size_t n, unsigned int) { return hipMalloc(p, n); }
-hipError_t hipHostFree(void *p) { return hipFree(p); }
+hipError_t hipHostMalloc(void **p, size_t n, unsigned int) {
+    *p = aligned_alloc(256, (n + 255) & ~size_t(255));
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostFree(void *p) {
+    free(p);
+    return hipSuccess;
+}
 hipError_t hipHostRegister(void *, size_t, unsigned int) { return hipSuccess; }
 hipError_t hipHostUnregister(void *) { return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int) {
@@ -121,11 +170,13 @@ hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
     return hipSuccess;
 }
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t st) {
+    check_op(st, {d, s});
     run_on(st, [=] { memcpy(d, s, n); });
     return hipSuccess;
 }
 hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int) {
     *s = new ihipStream_t();
+    (*s)->dev = t_device;
     std::lock_guard<std::mutex> lk(g_streams_mu);
     g_streams.push_back(*s);
     return hipSuccess;
@@ -197,6 +248,14 @@ hipError_t hipEventSynchronize(hipEvent_t e) {
     return hipSuccess;
 }
 const char *hipGetErrorString(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "fake hip error"; }
+
+// test hooks (multidev.cpp): windows computed per device since the last reset, routing violations
+void fakehip_reset(void) {
+    for (auto &w : g_windows) w = 0;
+    g_violations = 0;
+}
+int64_t fakehip_windows(int dev) { return dev >= 0 && dev < kMaxDev ? g_windows[dev].load() : -1; }
+int64_t fakehip_violations(void) { return g_violations.load(); }
 }  // extern "C"
 
 // ---- kernel launch stubs (wsp_internal.h): record element k of window w = x_w[k % N] + k
@@ -220,6 +279,7 @@ int64_t record_of(int n, int output, int topk) {
 }  // namespace
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t s) {
+    check_op(s, {L.series, L.out, L.twiddle}, L.n_windows);
     const SpectrumLaunch c = L;
     run_on(s, [c] {
         const int n = 1 << c.log2n;
@@ -231,11 +291,13 @@ hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t s) {
 }
 hipError_t launch_spectrum_f32(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
 hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {  // hop = 1 top-k records, same record function
+    check_op(s, {a.series, a.out}, a.n_windows);
     const SlideArgs c = a;
     run_on(s, [c] { fill<double>(c.series, 1, 1 << c.log2n, c.n_windows, 4 * c.topk, c.out); });
     return hipSuccess;
 }
 hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {  // hop = 1 power rows, same record function
+    check_op(s, {a.series, a.out}, a.n_windows);
     const SlideArgs c = a;
     run_on(s, [c] {
         const int n = 1 << c.log2n;
@@ -246,6 +308,7 @@ hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {  // hop = 1 power r
 }
 hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // detrended = the window itself
+    check_op(s, {L.series, L.detrended});
     const KalmanLaunch c = L;
     run_on(s, [c] {
         const size_t es = c.f32 ? 4 : 8;
@@ -256,6 +319,7 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // det
     return hipSuccess;
 }
 hipError_t launch_inverse(const InverseLaunch &L, hipStream_t s) {
+    check_op(s, {L.in, L.out}, L.n_windows);
     const InverseLaunch c = L;
     run_on(s, [c] { fill<double>(c.in, int64_t(1) << c.log2n, 1 << c.log2n, c.n_windows, int64_t(1) << c.log2n, c.out); });
     return hipSuccess;
@@ -265,6 +329,7 @@ hipError_t launch_phase_row(const double *spec, int n_bins, int, double *out, hi
     return hipSuccess;
 }
 hipError_t launch_large(const LargeLaunch &L, hipStream_t s) {
+    check_op(s, {L.series, L.out}, L.n_windows);
     const LargeLaunch c = L;
     run_on(s, [c] {
         const int n = 1 << c.log2n;

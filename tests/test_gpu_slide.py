@@ -86,11 +86,12 @@ def test_slide_segment_seams(gpu_session, nwin):
     plan.close()
 
 
-@pytest.mark.parametrize("seg", [0, 1366])
+@pytest.mark.parametrize("seg", [0, 1366, 2048])
 def test_slide_vs_fft_large_segments(gpu_session, seg):
-    """The C4 batch (1,048,576 windows; default segments, or 1366-window segments = three 512-step
-    staging chunks each): slide against the FFT kernel on the same buffer, every window; the oracle on
-    the windows around every 37th 512-window boundary."""
+    """The C4 batch (1,048,576 windows; default segments, 1366-window segments = three 512-step
+    staging chunks each, or the longest segment wsp_plan_set_slide_segment accepts): slide against the
+    FFT kernel on the same buffer, every window; the oracle on the windows around every 37th
+    512-window boundary."""
     torch = pytest.importorskip("torch")
     n, nwin = 2048, 1_048_576
     dev = torch.device("cuda", 0)
@@ -307,3 +308,39 @@ def test_slide_topk_host_batch_path(gpu_session):
     spec = oracle.batch_spectrum(s, n, 1, "mean", "hann")
     kmin, kmax = oracle.band(n)
     _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
+@pytest.mark.parametrize("kind", ["slide_topk", "kalman"])
+def test_stateful_plan_on_two_streams(gpu_session, kind):
+    """One plan with a device workspace (hop = 1 top-k segment seeds; Kalman pre-pass windows) executed
+    back to back on two streams from the same thread, on different inputs: wsp_plan_execute orders the
+    second after the first on the device (no host sync), so neither execute sees the other's workspace
+    contents -- both results equal the plan's results for the same inputs run alone."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    if kind == "slide_topk":
+        n, nwin, hop = 2048, 60000, 1
+        plan = bridge.Plan(0, n, hop, nwin, "none", "hann", output="topk")
+        plan.set_topk(8, 18.0, 200.0)
+        assert plan.algorithm() == "slide"
+    else:
+        n, nwin, hop = 1024, 4096, 1024
+        plan = bridge.Plan(0, n, hop, nwin, "kalman", "hann")
+    length = (nwin - 1) * hop + n
+    ins = [synth.random_walk_torch(length, 100 + i, dev) for i in range(2)]
+    alone = []
+    for x in ins:
+        o = torch.empty(nwin * plan.record, dtype=torch.float64, device=dev)
+        plan.execute(x.data_ptr(), o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        alone.append(o)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs = [torch.empty_like(alone[0]).fill_(float("nan")) for _ in range(2)]
+    torch.cuda.synchronize()
+    for rep in range(3):  # several interleavings: A, B, A, B, ...
+        for i in range(2):
+            plan.execute(ins[i].data_ptr(), outs[i].data_ptr(), streams[i].cuda_stream)
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(outs[i], alone[i]), (kind, i)
+    plan.close()

@@ -35,3 +35,17 @@ def test_host_layer_under_sanitizer(built, san):
     assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out, out[-4000:]
     assert "runtime error" not in out, out[-4000:]
     assert r.returncode == 0 and "hostsan stress: ok" in out, out[-4000:]
+
+
+@pytest.mark.parametrize("devices", [2, 8])
+@pytest.mark.parametrize("san", ["tsan", "asan"])
+def test_multi_device_sharding_under_sanitizer(built, san, devices):
+    """gpu_init(-1) over 2 and 8 fake devices (multidev.cpp): every record of sharded batches (halo,
+    disjoint output ranges), the per-device window split, per-device streams and buffers, 8 charts
+    polling sharded jobs at once -- clean under TSAN and ASAN+UBSAN."""
+    r = subprocess.run([str(built / f"multidev_{san}"), str(built / f"libmtbridge_{san}.so"), str(devices)],
+                       capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out, out[-4000:]
+    assert "runtime error" not in out, out[-4000:]
+    assert r.returncode == 0 and f"hostsan multidev {devices}: ok" in out, out[-4000:]

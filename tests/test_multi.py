@@ -142,3 +142,41 @@ def test_bench_world_size_mismatch_fails():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r, lines = _bench_line("--gpus", "2", "--plan-only", env=env)
     assert r.returncode != 0 and not lines and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_gpus8_c4_strong_plan():
+    """The driver's 8-GPU shape (--gpus 8 --config c4 --scaling strong) rehearsed on a real 8-rank gloo
+    rendezvous without a GPU: contiguous window ranges covering the 1,048,576 windows exactly once, each
+    rank's series slice = its windows plus the N - hop halo, neighbours overlapping by exactly the halo."""
+    r, lines = _bench_line("--gpus", "8", "--config", "c4", "--scaling", "strong", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = lines
+    shards = line["shards"]
+    assert line["n_gpus"] == 8 and [s["rank"] for s in shards] == list(range(8))
+    n, hop, W = 2048, 1, 1048576
+    assert sum(s["windows"] for s in shards) == W and shards[0]["w0"] == 0
+    for a, b in zip(shards, shards[1:]):
+        assert b["w0"] == a["w0"] + a["windows"]
+        assert a["series"][1] - b["series"][0] == n - hop
+    for s in shards:
+        assert s["windows"] == W // 8 and s["seed"] == 13  # one batch (same series) split evenly
+        assert s["series"] == [s["w0"] * hop, (s["w0"] + s["windows"] - 1) * hop + n]
+
+
+def test_bench_gpus8_c5_and_weak_plans():
+    """C5 over 8 ranks (whole symbols, balanced by output bytes within 10 %) and the weak-scaling north star
+    (every rank a full 65536-window batch of its own seed)."""
+    r, lines = _bench_line("--gpus", "8", "--config", "c5", "--scaling", "strong", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = lines
+    syms = sorted(s for sh in line["shards"] for s in sh["symbols"])
+    assert syms == list(range(28))
+    lens = (512, 1024, 2048, 4096)
+    out_bytes = [sum((20000 - lens[s // 7] + 1) * lens[s // 7] // 2 for s in sh["symbols"]) for sh in line["shards"]]
+    assert min(out_bytes) > 0 and max(out_bytes) / min(out_bytes) < 1.10
+    r, lines = _bench_line("--gpus", "8", "--config", "north_star", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = lines
+    assert line["scaling"] == "weak"
+    assert [s["windows"] for s in line["shards"]] == [65536] * 8
+    assert len({s["seed"] for s in line["shards"]}) == 8
