@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
                     help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
     ap.add_argument("--c5-streams", type=int, default=3, help="C5: streams the symbol plans are spread over")
+    ap.add_argument("--c5-mode", default="group", choices=["group", "plans"],
+                    help="C5: one grouped device plan (wsp_group_*: one launch per window length) or one plan per "
+                         "symbol spread over --c5-streams streams (round-2 form, ablation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
@@ -349,10 +352,13 @@ class SingleBatch(Workload):
 class C5Batch(Workload):
     """C5: 28 symbols x 20000 bars, N in {512,1024,2048,4096} (7 symbols each), hop = 1, fp64,
     Hann -- the WaveCyclesBatchFetcher shape (WaveCyclesBatchFetcher.mq5:106-133: one batch per
-    symbol).  One step = every owned symbol's batch; each window length runs on its own stream,
-    joined into the launch stream."""
+    symbol).  One step = every owned symbol's batch.  Default (--c5-mode group): one grouped device
+    plan (wsp_group_*), the symbols of each window length in one sliding-DFT launch on the launch
+    stream.  --c5-mode plans: one plan per symbol, spread over --c5-streams streams joined into the
+    launch stream (the round-2 form)."""
 
-    def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0, c5_layout="greedy", c5_streams=3):
+    def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0, c5_layout="greedy", c5_streams=3,
+                 c5_mode="group"):
         import torch
         from wavespec_amd import bridge, synth
         dev = torch.device("cuda", local_rank)
@@ -360,6 +366,27 @@ class C5Batch(Workload):
         nwins = [bars - lens[s // 7] + 1 for s in range(28)]
         sp = shard_plan("c5", rank, world, scaling)
         owned, seed_off = sp["symbols"], sp["seed_offset"]
+        self.f32 = False
+        self.stream = torch.cuda.current_stream(dev)
+        self.group = None
+        self.describe = (f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2"
+                         + (f", {len(owned)} symbols on this rank" if scaling == "strong" else ""))
+        if c5_mode == "group" and algo in ("auto", "slide") and not slide_seg:
+            self.series = [synth.random_walk_torch(bars, 100 + sym + seed_off, dev) for sym in owned]
+            self.outs = [torch.empty(nwins[sym] * (lens[sym // 7] // 2), dtype=torch.float64, device=dev)
+                         for sym in owned]
+            self.group = bridge.Group(local_rank, [lens[sym // 7] for sym in owned], [nwins[sym] for sym in owned])
+            self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
+            self.algorithm = "slide-group"
+            self.layout = {"mode": "group", "launches": self.group.launches}
+            self.windows = sum(nwins[sym] for sym in owned)
+            self.alg_bytes = self.group.algorithmic_bytes
+            self.traffic = load_traffic("c5")
+            i4 = [i for i, sym in enumerate(owned) if lens[sym // 7] == 4096]
+            if i4:
+                self.cpu_cfg = (self.series[i4[-1]], {"n": 4096, "hop": 1, "windows": nwins[owned[i4[-1]]],
+                                                      "detrend": "none", "window": "hann"})
+            return
         # Three streams, within the box's 4 HIP hardware queues together with the launch stream (with
         # one stream per length two of them shared a hardware queue and ran 14 kernels back to back:
         # the whole step, profiles/r02/c5_kernel_stats.csv).  --c5-layout: "length" puts {4096}, {2048},
@@ -396,20 +423,18 @@ class C5Batch(Workload):
                 plan.set_slide_segment(slide_seg)
             self.jobs.append((plan, series, out, self.streams[assign[sym]]))
         self.algorithm = "+".join(sorted({j[0].algorithm() for j in self.jobs}))
-        self.stream = torch.cuda.current_stream(dev)
         self.windows = sum(j[0].n_windows for j in self.jobs)
         self.alg_bytes = sum(j[0].algorithmic_bytes for j in self.jobs)
-        per_launch = load_traffic("c5" if algo == "auto" else f"c5_{algo}")  # PMC bytes per spectrum dispatch; one step is len(jobs) dispatches
-        self.traffic = per_launch * len(self.jobs) if per_launch else None
-        self.f32 = False
+        self.traffic = load_traffic("c5_plans" if algo == "auto" else f"c5_{algo}")  # PMC bytes per step (28 plans)
         big = [j for j in self.jobs if j[0].window_len == 4096]
         if big:  # a 4096-pt symbol: the costliest per window
             p0, s0 = big[-1][0], big[-1][1]
             self.cpu_cfg = (s0, {"n": 4096, "hop": 1, "windows": p0.n_windows, "detrend": "none", "window": "hann"})
-        self.describe = (f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2"
-                         + (f", {len(owned)} symbols on this rank" if scaling == "strong" else ""))
 
     def step(self):
+        if self.group is not None:
+            self.group.execute(*self._ptrs, self.stream.cuda_stream)
+            return
         for st in self.streams:
             st.wait_stream(self.stream)
         for plan, series, out, st in self.jobs:
@@ -418,6 +443,9 @@ class C5Batch(Workload):
             self.stream.wait_stream(st)
 
     def close(self):
+        if self.group is not None:
+            self.group.close()
+            return
         for j in self.jobs:
             j[0].close()
 
@@ -448,7 +476,8 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     ctl = Control(world)
     if args.config == "c5":
-        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.c5_layout, args.c5_streams)
+        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.c5_layout, args.c5_streams,
+                     args.c5_mode)
     else:
         wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
     torch.cuda.synchronize()

@@ -36,6 +36,12 @@ struct KP {
     double follow, qp, qv, qa, qj, adapt, r, vp, vv, va, vj, iv, ia, ij, clip, ema;
 };
 
+// The filter state is re-centred on a sample every kRecentre steps (see kalman_detrend_kernel): at
+// most this many steps carry a level move (a price jump) in pos before it is shifted out.  Every
+// segment start and tile length is a multiple of it, so segments that meet at a hand-over sit on the
+// same centre.
+constexpr int kRecentre = 16;
+
 // 1/sqrt: hardware v_rsq_f32 for the fp32 filter (1 ulp), exact for fp64
 __device__ __forceinline__ float krsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ double krsqrt(double x) { return 1.0 / sqrt(x); }
@@ -360,7 +366,8 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
 #pragma unroll
             for (int j = 0; j < J; ++j) zrow[j] = tile[lr * (J + 1) + j];
             // re-centre on the tile's first sample (shift-equivariance: only pos and the EMA carry the
-            // level); the shift base - zrow[0] is exact for prices within 2x of each other (Sterbenz)
+            // level) and every kRecentre samples after it; the shift base - zrow[j] is exact for prices
+            // within 2x of each other (Sterbenz)
             if (c == 0) {
                 kreset<K>(st, kp, K(0));
             } else {
@@ -371,7 +378,13 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_detrend_kernel(const T *__r
             base = zrow[0];
 #pragma unroll UNROLL
             for (int j = 0; j < J; ++j) {
-                const K z = (K)(zrow[j] - base);  // exact for prices within 2x of the tile's first (Sterbenz)
+                if (j > 0 && j % kRecentre == 0) {  // and every kRecentre steps inside the tile
+                    const K sh = (K)(base - zrow[j]);
+                    st.pos += sh;
+                    st.ema_prev += sh;
+                    base = zrow[j];
+                }
+                const K z = (K)(zrow[j] - base);  // exact for prices within 2x of the centre (Sterbenz)
                 const K trend = kstep<K, TWO, PKUP>(st, kc, z);
                 zrow[j] = T(z - trend);
             }
@@ -625,12 +638,13 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 zrow[j] = kf2{v.x, v.y};
                 zrow[j + 1] = kf2{v.z, v.w};
             }
-            // Re-centre both segments on their tile's first sample.  StepKalman4D is exactly
-            // shift-equivariant (only pos carries the level: innovation, gain, boost and clip see
-            // differences), so moving the centre is exact up to one rounding of pos per tile, and
-            // pos stays at the size of the local excursion instead of the distance from sample 0:
-            // a 0.5 level jump inside a window then costs fp32 no precision (2e-5 -> 1e-6 of the
-            // spectrum, scripts/kalman_f32_emulation.py).  base - zrow[0] is exact (Sterbenz).
+            // Re-centre both segments on a sample every kRecentre steps (the tile's first, then
+            // inside the tile).  StepKalman4D is exactly shift-equivariant (only pos carries the
+            // level: innovation, gain, boost and clip see differences), so moving the centre is
+            // exact up to one rounding of pos per move, and pos stays at the size of the local
+            // excursion instead of the distance from sample 0: a 0.5 level jump inside a window
+            // then costs fp32 ~20x less (2-4e-5 -> 1-3e-6 of the spectrum,
+            // scripts/kalman_f32_emulation.py).  base - zrow[j] is exact (Sterbenz).
             if (c == 0) {  // (sample 0, sample L0 - WU): both segments reset at their first sample
                 KState<float> a;
                 kreset<float>(a, kp, 0.f);
@@ -644,7 +658,11 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
             base = zrow[0];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
-                const kf2 z = zrow[j] - base;  // exact for prices within 2x of the tile's first (Sterbenz)
+                if (j > 0 && j % kRecentre == 0) {  // and every kRecentre steps inside the tile
+                    st.pos += base - zrow[j];
+                    base = zrow[j];
+                }
+                const kf2 z = zrow[j] - base;  // exact for prices within 2x of the centre (Sterbenz)
                 const kf2 trend = kstep_pk2(st, kc, z);
                 zrow[j] = z - trend;
             }
@@ -678,7 +696,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     };
     run(0, nchunks, 0, WUC, std::true_type{});
     // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it.
-    // Both are centred on sample L0 - J: segment A's last tile is segment B's tile WUC - 1.
+    // Both are centred on sample L0 - kRecentre: segment A's last tile is segment B's tile WUC - 1.
     const float fl = 0x1p-24f * (fabsf(base.x) + fabsf(st.pos.x));
     const bool ok = kagree(st.pos.x, warm.pos, fl) && kagree(st.vel.x, warm.vel, fl) && kagree(st.acc.x, warm.acc, fl) &&
                     kagree(st.jerk.x, warm.jerk, fl) && kagree(st.p00.x, warm.p00, 0.f) && kagree(st.p01.x, warm.p01, 0.f) &&

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -452,6 +453,30 @@ bool use_slide_topk(const Config &c) {
     return c.algo == MTB_ALGO_SLIDE || c.n_windows >= 256;
 }
 
+// Launch constants of the sliding DFT for a configuration (tables on `dev`, window coefficients,
+// rotations); series / out / n_windows are the caller's.
+int slide_args(int dev, const Config &c, SlideArgs *A) {
+    Tables t64;
+    void *stab = nullptr;
+    int st;
+    if ((st = get_tables(dev, c.log2n, false, &t64)) != MTB_OK) return st;
+    if ((st = get_slide_table(dev, c.log2n, c.window, &stab)) != MTB_OK) return st;
+    HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    const WinCoef wc = window_coef(c.window);
+    const long double th = 2.0L * 3.141592653589793238462643383279502884L / (long double)(c.n - 1);
+    A->twiddle = t64.tw;
+    A->omega = stab;
+    A->seg = c.slide_seg;
+    A->log2n = c.log2n;
+    A->nf = wc.nf;
+    A->detrend = c.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
+    A->f32 = c.f32;
+    A->s0 = wc.a0, A->s1 = wc.a1 / 2, A->s2 = wc.a2 / 2;
+    A->c1 = (double)cosl(th), A->sn1 = (double)sinl(th), A->c2 = (double)cosl(2 * th), A->sn2 = (double)sinl(2 * th);
+    A->inv_n = 1.0 / c.n;
+    return MTB_OK;
+}
+
 // ------------------------------------------------------------ device path
 // series (device) -> [Kalman pre-pass into ws] -> spectrum kernel -> out.
 int enqueue(int dev, const Config &c, const double *kalman, const void *d_series, void *d_out, void *d_ws,
@@ -511,27 +536,11 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
     }
     if (use_slide(c) || use_slide_topk(c)) {
         const bool topk = use_slide_topk(c);
-        Tables t64;
-        void *stab = nullptr;
-        if ((st = get_tables(dev, c.log2n, false, &t64)) != MTB_OK) return st;
-        if ((st = get_slide_table(dev, c.log2n, c.window, &stab)) != MTB_OK) return st;
-        HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
-        const WinCoef wc = window_coef(c.window);
-        const long double th = 2.0L * 3.141592653589793238462643383279502884L / (long double)(c.n - 1);
         SlideArgs A{};
+        if ((st = slide_args(dev, c, &A)) != MTB_OK) return st;
         A.series = d_series;
         A.out = d_out;
-        A.twiddle = t64.tw;
-        A.omega = stab;
         A.n_windows = c.n_windows;
-        A.seg = c.slide_seg;
-        A.log2n = c.log2n;
-        A.nf = wc.nf;
-        A.detrend = c.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
-        A.f32 = c.f32;
-        A.s0 = wc.a0, A.s1 = wc.a1 / 2, A.s2 = wc.a2 / 2;
-        A.c1 = (double)cosl(th), A.sn1 = (double)sinl(th), A.c2 = (double)cosl(2 * th), A.sn2 = (double)sinl(2 * th);
-        A.inv_n = 1.0 / c.n;
         if (topk) {
             A.seg = slide_topk_seg(c);
             A.kmin = c.kmin;
@@ -1050,6 +1059,28 @@ std::unique_ptr<LiveCtx> live_checkout(Session &S, int n) {
 void live_checkin(Session &S, std::unique_ptr<LiveCtx> L) {
     std::lock_guard<std::mutex> lk(S.live_mu);
     S.live_free.push_back(std::move(L));
+}
+
+// ------------------------------------------------------------------ grouped hop = 1 plans
+// A multi-symbol hop = 1 batch -- the WaveCyclesBatchFetcher shape, one series per symbol
+// (WaveCyclesBatchFetcher.mq5:112-118), C5 = 28 symbols of 4 window lengths -- as one device plan:
+// the members of each window length run in ONE sliding-DFT launch (launch_slide_group: workgroup ->
+// (member, segment) table), longest windows first, on the caller's stream.  Against one plan per
+// symbol this removes the per-plan launches and, above all, the short per-plan segments: the segment
+// length follows the residency and the length's TOTAL window count, so a 19k-window symbol seeds its
+// trackers once per 128-256 windows instead of once per 32.  No workspace: executes may overlap.
+struct Group {
+    int dev = 0;
+    std::vector<Config> cfg;               // one per member (hop 1, power)
+    std::vector<std::vector<int>> launch;  // member indices per launch: one window length, <= kSlideGroupMax
+};
+std::mutex g_groups_mu;
+std::map<int64_t, std::shared_ptr<Group>> *g_groups = new std::map<int64_t, std::shared_ptr<Group>>();
+
+std::shared_ptr<Group> find_group(int64_t id) {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    auto it = g_groups->find(id);
+    return it == g_groups->end() ? nullptr : it->second;
 }
 
 }  // namespace
@@ -1683,6 +1714,94 @@ MTB_API int32_t wsp_plan_destroy(int64_t plan) {
     }
     p.reset();  // the last reference (here, or an execute in flight) retires the workspace
     ws_reap();
+    return MTB_OK;
+}
+
+MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_t *window_len, const int64_t *n_windows,
+                                 int32_t detrend, int32_t window, int32_t precision) {
+    if (!plan_device_ok(device)) return 0;
+    if (n_members < 1 || n_members > 4096 || !window_len || !n_windows) {
+        set_error("wsp_group_create: n_members=%d (1..4096) and non-null window_len / n_windows arrays needed", n_members);
+        return 0;
+    }
+    auto g = std::make_shared<Group>();
+    g->dev = device;
+    std::map<int, std::vector<int>, std::greater<int>> by_len;  // longest first
+    for (int m = 0; m < n_members; ++m) {
+        Config c;
+        if (make_config(window_len[m], 1, n_windows[m], detrend, window, 0, precision, MTB_OUT_POWER, &c) != MTB_OK) return 0;
+        if (!slide_eligible(c)) {
+            set_error("wsp_group_create: member %d (window_len=%d, detrend=%d, window=%d) is not a sliding-DFT batch "
+                      "(window_len 512..8192, detrend none / mean, Hann / Hamming / Blackman / none)",
+                      m, window_len[m], detrend, window);
+            return 0;
+        }
+        Tables t;
+        SlideArgs A{};
+        if (get_tables(device, c.log2n, c.f32, &t) != MTB_OK || slide_args(device, c, &A) != MTB_OK) return 0;
+        g->cfg.push_back(c);
+        by_len[c.n].push_back(m);
+    }
+    for (auto &kv : by_len)
+        for (size_t i = 0; i < kv.second.size(); i += kSlideGroupMax)
+            g->launch.emplace_back(kv.second.begin() + i,
+                                   kv.second.begin() + std::min(kv.second.size(), i + (size_t)kSlideGroupMax));
+    const int64_t id = g_next_id.fetch_add(1);
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    (*g_groups)[id] = std::move(g);
+    return id;
+}
+
+MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, void *const *d_out, void *hip_stream) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g) {
+        set_error("unknown group %lld", (long long)group);
+        return MTB_BAD_ARGS;
+    }
+    if (!d_series || !d_out) {
+        set_error("wsp_group_execute: null member array");
+        return MTB_BAD_ARGS;
+    }
+    for (size_t m = 0; m < g->cfg.size(); ++m)
+        if (!d_series[m] || !d_out[m]) {
+            set_error("wsp_group_execute: member %zu has a null device buffer", m);
+            return MTB_BAD_ARGS;
+        }
+    for (const auto &L : g->launch) {
+        SlideArgs A{};
+        const int st = slide_args(g->dev, g->cfg[L[0]], &A);
+        if (st != MTB_OK) return st;
+        SlideGroup G;
+        G.n = (int)L.size();
+        for (int i = 0; i < G.n; ++i) {
+            G.series[i] = d_series[L[i]];
+            G.out[i] = d_out[L[i]];
+            G.n_windows[i] = g->cfg[L[i]].n_windows;
+        }
+        HIP_OR(launch_slide_group(A, G, (hipStream_t)hip_stream), MTB_INTERNAL_ERROR);
+    }
+    return MTB_OK;
+}
+
+MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g) return -1;
+    int64_t b = 0;
+    for (const Config &c : g->cfg) b += (c.unique_input_elems() + c.n_windows * c.record()) * (int64_t)c.elem();
+    return b;
+}
+
+MTB_API int32_t wsp_group_launches(int64_t group) {
+    std::shared_ptr<Group> g = find_group(group);
+    return g ? (int32_t)g->launch.size() : -1;
+}
+
+MTB_API int32_t wsp_group_destroy(int64_t group) {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    if (!g_groups->erase(group)) {
+        set_error("unknown group %lld", (long long)group);
+        return MTB_BAD_ARGS;
+    }
     return MTB_OK;
 }
 

@@ -188,11 +188,31 @@ __device__ __forceinline__ void slide_step(d2 (&tr)[B][NF], const d2 (&om)[B][NF
     if constexpr (DETREND == kDetrendMean) sum += r[Rec<NF>::n - 1];
 }
 
+// Workgroup -> (member, segment) of a grouped launch (SlideGroup): members own contiguous runs of
+// workgroups.  Unrolled selects over the kernel-argument table (uniform scalar loads, no dynamic
+// indexing of the argument struct).
+struct SlideSeg {
+    const void *series;
+    void *out;
+    int64_t w0, n_windows;
+};
+__device__ __forceinline__ SlideSeg slide_seg_of(const SlideGroup &g, int64_t seg) {
+    const int64_t b = blockIdx.x;
+    SlideSeg r{g.series[0], g.out[0], b * seg, g.n_windows[0]};
+#pragma unroll
+    for (int i = 1; i < kSlideGroupMax; ++i)
+        if (i < g.n && b >= g.blk0[i]) r = SlideSeg{g.series[i], g.out[i], (b - g.blk0[i]) * seg, g.n_windows[i]};
+    return r;
+}
+
 template <typename T, int LOG2N, int NF, int DETREND>
 __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
-                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a) {
+                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a,
+                                                                                                              SlideGroup g) {
     constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B;
     constexpr int REC = Rec<NF>::n;
+    const SlideSeg sg = slide_seg_of(g, a.seg);  // this workgroup's member (a single plan is a group of one)
+    if (sg.w0 >= sg.n_windows) return;
     // per-step uniforms staged CH steps at a time: N/4 clamped to [128, 512], so that small windows keep
     // 4 single-/two-wave workgroups per SIMD (LDS: FFT buffer + quarter twiddles + uniforms)
     constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
@@ -203,10 +223,8 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
 
     const int t = threadIdx.x;
     auto kbin = [](int tt, int b) { return kbin_of<NT>(tt, b); };
-    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
-    if (w0 >= a.n_windows) return;
-    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
-    const T *__restrict__ x = static_cast<const T *>(a.series) + w0;
+    const int len = (int)((sg.n_windows - sg.w0) < a.seg ? (sg.n_windows - sg.w0) : a.seg);
+    const T *__restrict__ x = static_cast<const T *>(sg.series) + sg.w0;  // the segment's first window
     const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);  // [NF][M]
     const d2 *__restrict__ hwin = omega + NF * M;                      // [M]
 
@@ -244,7 +262,7 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
         sum = sum0;
     }
 
-    T *__restrict__ out = static_cast<T *>(a.out) + w0 * M + 2 * t;
+    T *__restrict__ out = static_cast<T *>(sg.out) + sg.w0 * M + 2 * t;
     double *u = reinterpret_cast<double *>(lds);
     for (int c0 = 0; c0 < len; c0 += CH) {
         const int clen = len - c0 < CH ? len - c0 : CH;
@@ -375,6 +393,165 @@ __global__ __launch_bounds__(64) void slide_topk_kernel(SlideArgs a) {
     }
 }
 
+// ---- the same records by a transposed scan (k <= 8): lane per window instead of a wave per window.
+// The wave slides its band's trackers as slide_topk_kernel does (lane l: bins kmin + l + 64 b) and
+// stages WB consecutive windows' band X in LDS ([window][bin], odd row stride: the scan's 16-byte
+// reads of 16 rows are conflict-free).  Then the lanes turn to the windows: lane l scans window
+// l % WB over the quarter (LPW = 64 / WB parts) l / WB of the band with the reference's 8-slot
+// insertion in registers (strict '>' against slots sorted by power: an equal power goes after the
+// earlier, lower bin -- L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554), and the
+// LPW partial lists of a window are merged across lanes (log2 LPW rounds: exchange with the partner
+// lane, keep the best 8 of the two by a bitonic merge under the key (power desc, bin asc)).  Every
+// lane of a window then holds its top 8; lane part q writes slots 2q, 2q + 1 (Re / Im from LDS).
+// Against one wave-wide max + ballot per slot and window (topk_wave64: 8 dependent reduction rounds
+// per window), the scan is ~90 independent VALU operations per window and lane group.
+constexpr int kTopkT = 8;  // slots of the transposed scan (the reference's top 8); larger k: slide_topk_kernel
+
+__device__ __forceinline__ bool kbetter(double pa, int ba, double pb, int bb) { return pa > pb || (pa == pb && ba < bb); }
+
+template <int LOG2N, int NF, int DETREND, int NB, int WB>
+__global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128, LPW = 64 / WB, K = kTopkT;
+    constexpr int SPMAX = (64 * NB) | 1;  // the widest band this NB serves, odd
+    constexpr int kEmpty = 0x7fffffff;    // bin of an empty slot: sorts after every real bin
+    __shared__ double u[CHT * REC];
+    __shared__ d2 xs[WB * SPMAX];
+    const int l = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
+    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
+    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
+    const d2 *__restrict__ hwin = omega + NF * M;
+    const d2 *__restrict__ ws = static_cast<const d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int span = a.span, kmin = a.kmin, sp = span | 1;
+    d2 tr[NB][NF], om[NB][NF], hk[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = l + 64 * b;
+        const bool ok = j < span;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            tr[b][f] = ok ? ws[f * span + j] : d2{0.0, 0.0};
+            om[b][f] = ok ? omega[f * M + kmin + j] : d2{1.0, 0.0};
+        }
+        hk[b] = (DETREND == kDetrendMean && ok) ? hwin[kmin + j] : d2{0.0, 0.0};
+    }
+    const d2 sl = ws[NF * span];
+    double sum = sl.x;
+    const double lvl = sl.y;
+    // the scan's lane roles: window mw of the staged batch, band part mq: bins [q0, q1)
+    const int mw = l % WB, mq = l / WB;
+    const int qs = (span + LPW - 1) / LPW, q0 = mq * qs, q1 = q0 + qs < span ? q0 + qs : span;
+    double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
+    const int kk = a.topk;
+    for (int c0 = 0; c0 < len; c0 += CHT) {
+        const int clen = len - c0 < CHT ? len - c0 : CHT;
+        if (c0) __syncthreads();
+        stage_uniforms<double, NF, N>(a, x, lvl, c0, clen, len, u, l, 64);
+        __syncthreads();
+#pragma unroll 1
+        for (int st = 0; st < clen; ++st) {
+            const int wi = c0 + st, slot = wi % WB;
+            const double mwv = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                d2 X = tr[b][0];
+#pragma unroll
+                for (int f = 1; f < NF; ++f) X += tr[b][f];
+                if constexpr (DETREND == kDetrendMean) X -= mwv * hk[b];
+                const int j = l + 64 * b;
+                if (j < span) xs[slot * sp + j] = X;
+            }
+            if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
+            if (slot != WB - 1 && wi + 1 < len) continue;
+            // ---- scan the staged batch: windows wi - slot .. wi
+            __syncthreads();
+            double tp[K];
+            int tb[K];
+#pragma unroll
+            for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
+            const bool wok = mw <= slot;
+            if (wok) {
+                const d2 *row = xs + mw * sp;
+                for (int j = q0; j < q1; ++j) {
+                    const d2 X = row[j];
+                    const double p = X.x * X.x + X.y * X.y;
+                    // insertion as the reference: first slot s with p > tp[s] takes it, the rest shift down
+                    bool c[K];
+#pragma unroll
+                    for (int s = 0; s < K; ++s) c[s] = p > tp[s];
+#pragma unroll
+                    for (int s = K - 1; s > 0; --s) {
+                        tp[s] = c[s] ? (c[s - 1] ? tp[s - 1] : p) : tp[s];
+                        tb[s] = c[s] ? (c[s - 1] ? tb[s - 1] : j) : tb[s];
+                    }
+                    tp[0] = c[0] ? p : tp[0];
+                    tb[0] = c[0] ? j : tb[0];
+                }
+            }
+            // merge the LPW partial lists of a window (lanes mw + WB q): keep the best 8 of each pair
+#pragma unroll
+            for (int r = 1; r < LPW; r <<= 1) {
+                double op[K];
+                int ob[K];
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    op[s] = __shfl_xor(tp[s], WB * r, 64);
+                    ob[s] = __shfl_xor(tb[s], WB * r, 64);
+                }
+                // best of mine[s] and the partner's [K-1-s]: the 8 best of the union, in bitonic order
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    const bool t = kbetter(op[K - 1 - s], ob[K - 1 - s], tp[s], tb[s]);
+                    tp[s] = t ? op[K - 1 - s] : tp[s];
+                    tb[s] = t ? ob[K - 1 - s] : tb[s];
+                }
+                // bitonic half-cleaners: best first
+#pragma unroll
+                for (int h = K / 2; h > 0; h >>= 1)
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        if ((i & h) == 0) {
+                            const bool t = kbetter(tp[i + h], tb[i + h], tp[i], tb[i]);
+                            const double pa = tp[i], pb = tp[i + h];
+                            const int ba = tb[i], bb = tb[i + h];
+                            tp[i] = t ? pb : pa;
+                            tp[i + h] = t ? pa : pb;
+                            tb[i] = t ? bb : ba;
+                            tb[i + h] = t ? ba : bb;
+                        }
+            }
+            // records of window (wi - slot + mw): part mq writes slots mq * K / LPW ..
+            if (wok) {
+                double *o = rec + (int64_t)(wi - slot + mw) * (4 * kk);
+                constexpr int PER = K / LPW > 0 ? K / LPW : 1;
+#pragma unroll
+                for (int e = 0; e < PER; ++e) {
+                    const int s = mq * PER + e;
+                    // slot s of the lists by selects (register arrays are indexed at compile time only)
+                    double ps = tp[0];
+                    int bs = tb[0];
+#pragma unroll
+                    for (int i = 1; i < K; ++i) {
+                        ps = s == i ? tp[i] : ps;
+                        bs = s == i ? tb[i] : bs;
+                    }
+                    if (s < K && s < kk) {
+                        const bool real = bs != kEmpty;
+                        d2 X = d2{0.0, 0.0};
+                        if (real) X = xs[mw * sp + bs];
+                        typedef double d4 __attribute__((ext_vector_type(4)));
+                        *reinterpret_cast<d4 *>(o + 4 * s) =
+                            real ? d4{(double)(kmin + bs), ps, X.x, X.y} : d4{-1.0, -1.0, 0.0, 0.0};
+                    }
+                }
+            }
+            __syncthreads();  // the scan's reads before the next batch's writes
+        }
+    }
+}
+
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
     hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0, s,
@@ -382,6 +559,14 @@ template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideAr
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int nb = (a.span + 63) / 64;
+    // transposed scan for k <= 8 and bands of <= 256 bins (staged batch: WB windows x <= 64 NB bins); the
+    // 512-bin form (NB = 8: 80 tracker registers per lane) stays on the one-wave scan
+    if (a.topk <= kTopkT && a.variant == 0 && nb <= 4) {
+        if (nb <= 1) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 1, 16>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        else if (nb <= 2) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 2, 16>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 4, 8>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        return hipGetLastError();
+    }
     if (nb <= 1) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 1>), dim3((unsigned)grid), dim3(64), 0, s, a);
     else if (nb <= 2) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 2>), dim3((unsigned)grid), dim3(64), 0, s, a);
     else if (nb <= 4) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 4>), dim3((unsigned)grid), dim3(64), 0, s, a);
@@ -403,7 +588,12 @@ template <int LOG2N> hipError_t topk_by_nf(const SlideArgs &a, hipStream_t s) {
     }
 }
 
-template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const SlideArgs &a0, hipStream_t s) {
+// One launch over every member of the group: segment length from the residency (occupancy API, once
+// per instantiation) and the members' total window count, so that a multi-symbol batch gets the same
+// segments as one long series would (C5: 7 symbols of ~19k windows each seed 4-8x fewer times than
+// as separate launches).
+template <typename T, int LOG2N, int NF, int DETREND>
+hipError_t launch_t(const SlideArgs &a0, const SlideGroup &g0, hipStream_t s) {
     constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
     static std::atomic<int> resident{0};
     int res = resident.load(std::memory_order_relaxed);
@@ -418,36 +608,42 @@ template <typename T, int LOG2N, int NF, int DETREND> hipError_t launch_t(const 
         resident.store(res, std::memory_order_relaxed);
     }
     SlideArgs a = a0;
+    SlideGroup g = g0;
+    int64_t total = 0;
+    for (int m = 0; m < g.n; ++m) total += g.n_windows[m];
     if (a.seg <= 0) {  // ~2 rounds of resident workgroups, 32..256 windows each (sweep: DESIGN.md 4.5)
-        a.seg = (a.n_windows + 2 * (int64_t)res - 1) / (2 * (int64_t)res);
+        a.seg = (total + 2 * (int64_t)res - 1) / (2 * (int64_t)res);
         a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
     }
-    const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
-    hipLaunchKernelGGL((slide_kernel<T, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    g.blk0[0] = 0;
+    for (int m = 0; m < g.n; ++m) g.blk0[m + 1] = g.blk0[m] + (g.n_windows[m] + a.seg - 1) / a.seg;
+    const int64_t grid = g.blk0[g.n];
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL((slide_kernel<T, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a, g);
     return hipGetLastError();
 }
 
-template <typename T, int LOG2N, int NF> hipError_t by_detrend(const SlideArgs &a, hipStream_t s) {
-    return a.detrend == kDetrendMean ? launch_t<T, LOG2N, NF, kDetrendMean>(a, s)
-                                     : launch_t<T, LOG2N, NF, kDetrendNone>(a, s);
+template <typename T, int LOG2N, int NF> hipError_t by_detrend(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
+    return a.detrend == kDetrendMean ? launch_t<T, LOG2N, NF, kDetrendMean>(a, g, s)
+                                     : launch_t<T, LOG2N, NF, kDetrendNone>(a, g, s);
 }
 
-template <typename T, int LOG2N> hipError_t by_nf(const SlideArgs &a, hipStream_t s) {
+template <typename T, int LOG2N> hipError_t by_nf(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
     switch (a.nf) {
-    case 1: return by_detrend<T, LOG2N, 1>(a, s);
-    case 3: return by_detrend<T, LOG2N, 3>(a, s);
-    case 5: return by_detrend<T, LOG2N, 5>(a, s);
+    case 1: return by_detrend<T, LOG2N, 1>(a, g, s);
+    case 3: return by_detrend<T, LOG2N, 3>(a, g, s);
+    case 5: return by_detrend<T, LOG2N, 5>(a, g, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-template <typename T> hipError_t by_n(const SlideArgs &a, hipStream_t s) {
+template <typename T> hipError_t by_n(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
     switch (a.log2n) {
-    case 9: return by_nf<T, 9>(a, s);
-    case 10: return by_nf<T, 10>(a, s);
-    case 11: return by_nf<T, 11>(a, s);
-    case 12: return by_nf<T, 12>(a, s);
-    case 13: return by_nf<T, 13>(a, s);
+    case 9: return by_nf<T, 9>(a, g, s);
+    case 10: return by_nf<T, 10>(a, g, s);
+    case 11: return by_nf<T, 11>(a, g, s);
+    case 12: return by_nf<T, 12>(a, g, s);
+    case 13: return by_nf<T, 13>(a, g, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -471,9 +667,20 @@ hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {
 
 hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {
     if (a.n_windows <= 0) return hipSuccess;
-    if (a.log2n < kSlideMinLog2N || a.log2n > kSlideMaxLog2N)
+    SlideGroup g;
+    g.n = 1;
+    g.series[0] = a.series;
+    g.out[0] = a.out;
+    g.n_windows[0] = a.n_windows;
+    return launch_slide_group(a, g, s);
+}
+
+hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
+    if (g.n < 1 || g.n > kSlideGroupMax || a.log2n < kSlideMinLog2N || a.log2n > kSlideMaxLog2N)
         return hipErrorInvalidValue;
-    return a.f32 ? by_n<float>(a, s) : by_n<double>(a, s);
+    for (int m = 0; m < g.n; ++m)
+        if (g.n_windows[m] < 0 || !g.series[m] || !g.out[m]) return hipErrorInvalidValue;
+    return a.f32 ? by_n<float>(a, g, s) : by_n<double>(a, g, s);
 }
 
 }  // namespace wsp

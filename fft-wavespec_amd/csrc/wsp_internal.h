@@ -122,8 +122,23 @@ struct SlideArgs {
     // top-k records (launch_slide_topk, fp64): bins [kmin, kmin + span), topk slots, seeds workspace
     int kmin, span, topk;
     void *ws;             // ceil(n_windows / seg) * slide_topk_seed_stride(nf, span) double complex
+    int variant;          // top-k scan: 0 = transposed (lane per window, k <= 8), 1 = one wave per window
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
+// Grouped launch: several series of the same window length (the symbols of one length in a
+// WaveCyclesBatchFetcher-shaped multi-symbol batch, WaveCyclesBatchFetcher.mq5:112-118) in ONE
+// slide_kernel launch.  Member m owns workgroups [blk0[m], blk0[m + 1]); a workgroup's segment is
+// windows [(blockIdx - blk0[m]) * seg, ...) of member m.  a.series / a.out / a.n_windows are ignored;
+// a.seg = 0 takes the launcher's policy over the members' total window count.
+constexpr int kSlideGroupMax = 16;
+struct SlideGroup {
+    int n = 0;
+    const void *series[kSlideGroupMax];
+    void *out[kSlideGroupMax];
+    int64_t n_windows[kSlideGroupMax];
+    int64_t blk0[kSlideGroupMax + 1];  // filled by the launcher
+};
+hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream_t stream);
 // hop = 1 top-k records ([bin, power, Re, Im] x topk per window, MTB_OUT_TOPK) by the sliding DFT: the
 // band's trackers only (span <= 512), one wave per segment, the FFT kernel's one-wave scan per window.
 constexpr int kSlideTopkMaxSpan = 512;

@@ -73,6 +73,12 @@ SIGNATURES = {
     "wsp_plan_execute": (C.c_int32, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "wsp_plan_algorithmic_bytes": (C.c_int64, [C.c_int64]),
     "wsp_plan_destroy": (C.c_int32, [C.c_int64]),
+    "wsp_group_create": (C.c_int64, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32,
+                                     C.c_int32, C.c_int32]),
+    "wsp_group_execute": (C.c_int32, [C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_void_p]),
+    "wsp_group_algorithmic_bytes": (C.c_int64, [C.c_int64]),
+    "wsp_group_launches": (C.c_int32, [C.c_int64]),
+    "wsp_group_destroy": (C.c_int32, [C.c_int64]),
     "wsp_version": (C.c_char_p, []),
 }
 
@@ -323,6 +329,50 @@ class Plan:
     def close(self) -> None:
         if self.handle:
             lib().wsp_plan_destroy(self.handle)
+            self.handle = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Group:
+    """Grouped hop = 1 device plan (wsp_group_*): one series per symbol, every window of each
+    (the WaveCyclesBatchFetcher shape); the members of a window length run in one launch."""
+
+    def __init__(self, device: int, window_lens, n_windows, detrend="none", window="hann", precision="f64"):
+        lens = (C.c_int32 * len(window_lens))(*window_lens)
+        nws = (C.c_int64 * len(n_windows))(*n_windows)
+        if len(window_lens) != len(n_windows):
+            raise ValueError("one window length and one window count per member")
+        self.handle = lib().wsp_group_create(device, len(window_lens), lens, nws, DETREND[detrend], WINDOW[window],
+                                             PRECISION[precision])
+        if self.handle == 0:
+            raise BridgeError("wsp_group_create", BAD_ARGS, last_error())
+        self.window_lens, self.n_windows = list(window_lens), list(n_windows)
+
+    @property
+    def algorithmic_bytes(self) -> int:
+        return int(lib().wsp_group_algorithmic_bytes(self.handle))
+
+    @property
+    def launches(self) -> int:
+        return int(lib().wsp_group_launches(self.handle))
+
+    def execute(self, d_series, d_out, stream: int = 0) -> None:
+        """d_series / d_out: device pointers (ints), one per member."""
+        n = len(self.window_lens)
+        if len(d_series) != n or len(d_out) != n:
+            raise ValueError(f"{n} members: one series and one output pointer each")
+        ins = (C.c_void_p * n)(*d_series)
+        outs = (C.c_void_p * n)(*d_out)
+        _check("wsp_group_execute", lib().wsp_group_execute(self.handle, ins, outs, C.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self.handle:
+            lib().wsp_group_destroy(self.handle)
             self.handle = 0
 
     def __del__(self):

@@ -305,6 +305,28 @@ MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
  * + output, for roofline accounting. */
 MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan);
 
+/* Grouped hop = 1 plan: a multi-symbol batch in the WaveCyclesBatchFetcher
+ * shape (one series per symbol, WaveCyclesBatchFetcher.mq5:112-118; C5 = 28
+ * symbols x 4 window lengths) on device-resident buffers.  Member m: a series
+ * of n_windows[m] + window_len[m] - 1 samples, every window of it (hop = 1),
+ * MTB_OUT_POWER rows of window_len[m]/2 elements.  The members of each window
+ * length run in one sliding-DFT launch (longest windows first, up to 16
+ * members per launch), segmented over the length's total window count.
+ * Members must be sliding-DFT batches: window_len 512..8192, detrend none or
+ * mean, Hann / Hamming / Blackman / no window (Blackman up to 4096).  Returns
+ * a handle > 0, or 0 (see gpu_get_last_error_w). */
+MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_t *window_len,
+                                 const int64_t *n_windows, int32_t detrend, int32_t window, int32_t precision);
+/* Enqueues every member on `hip_stream`: d_series[m] / d_out[m] are device
+ * pointers (double or float per the precision).  Asynchronous, no host sync;
+ * a group has no workspace, so executes may run concurrently. */
+MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, void *const *d_out, void *hip_stream);
+/* Algorithmic bytes of one execute (sum over members, as wsp_plan_algorithmic_bytes). */
+MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
+/* Kernel launches one execute makes (one per window length and 16 members). */
+MTB_API int32_t wsp_group_launches(int64_t group);
+MTB_API int32_t wsp_group_destroy(int64_t group);
+
 MTB_API int32_t wsp_plan_destroy(int64_t plan);
 
 /* Version string "mtbridge-mi355x <semver> gfx950" (static storage). */

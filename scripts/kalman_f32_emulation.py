@@ -3,7 +3,7 @@
 Emulates the device's fp32 filter (two-stage predict, normalised update, kalman_core.h kstep_pk2)
 in numpy float32 with two centring policies:
   x0    state centred on the window's first sample (rounds 1-2)
-  tile  re-centred on the first sample of every 32-step LDS tile (round 3, the device default)
+  tile  re-centred on a sample every J = 16 steps (round 3, the device default: kalman_core.h kRecentre)
 and prints the spectrum error of each against the fp64 oracle filter (oracle.numpy_kalman_trend).
 A 0.5 level jump costs the x0 form 1.7e-5 - 3.8e-5; the tile form stays near 1e-6.
   python3 scripts/kalman_f32_emulation.py
@@ -19,7 +19,7 @@ import oracle  # noqa: E402
 from wavespec_amd import synth  # noqa: E402
 
 
-def device_f32_filter(X32, mode="tile", J=32):
+def device_f32_filter(X32, mode="tile", J=16):
     """Detrended windows d = z - trend of the device-form fp32 filter (reference default flags)."""
     (follow, q_pos, q_vel, q_acc, q_jerk, adapt, R, vp, vv, va, vj, iv, ia, ij, clip, _ema) = oracle.KALMAN_DEFAULTS
     f = np.float32

@@ -32,8 +32,11 @@ for r in rows("trace/**/*kernel_stats.csv"):
 
 
 def main_per_step(cfg):
-    """Main-kernel dispatches per bench step: 1, or the chunk count of the four-step large-N path
-    (one row_kernel per chunk of windows, csrc/large_fft.hip large_chunk: 192 MiB of column results)."""
+    """Main-kernel dispatches per bench step: 1, the chunk count of the four-step large-N path
+    (one row_kernel per chunk of windows, csrc/large_fft.hip large_chunk: 192 MiB of column results),
+    or C5's launches."""
+    if cfg == "c5":  # grouped plan: one slide launch per window length; per-symbol plans: 28 launches
+        return 28 if key.endswith(("_plans", "_fft")) else 4
     sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "fft-wavespec_amd"))
     from wavespec_amd import synth
     c = synth.CONFIGS.get(cfg)

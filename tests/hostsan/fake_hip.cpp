@@ -306,6 +306,24 @@ hipError_t launch_slide(const SlideArgs &a, hipStream_t s) {  // hop = 1 power r
     });
     return hipSuccess;
 }
+hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
+    int64_t total = 0;
+    for (int m = 0; m < g.n; ++m) {
+        check_op(s, {g.series[m], g.out[m]});
+        total += g.n_windows[m];
+    }
+    check_op(s, {}, total);
+    const SlideArgs c = a;
+    const SlideGroup gg = g;
+    run_on(s, [c, gg] {
+        const int n = 1 << c.log2n;
+        for (int m = 0; m < gg.n; ++m) {
+            if (c.f32) fill<float>(gg.series[m], 1, n, gg.n_windows[m], n / 2, gg.out[m]);
+            else fill<double>(gg.series[m], 1, n, gg.n_windows[m], n / 2, gg.out[m]);
+        }
+    });
+    return hipSuccess;
+}
 hipError_t launch_spectrum_phase(const SpectrumLaunch &L, hipStream_t s) { return launch_spectrum(L, s); }
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // detrended = the window itself
     check_op(s, {L.series, L.detrended});

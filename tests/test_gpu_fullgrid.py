@@ -285,3 +285,47 @@ def test_c5_28_symbols_concurrent(gpu_session):
     # the fixture's own reference still holds the session
     s = synth.random_walk(8 * 512, seed=1)
     assert oracle.rel_err(bridge.spectrum_batch(s, 512, 512), oracle.batch_spectrum(s, 512, 512)) <= 1e-10
+
+
+def test_c5_grouped_plan(gpu_session):
+    """C5 as benchmarked (bench.py --config c5): one grouped device plan over the 28 symbols
+    (wsp_group_*: the 7 symbols of each window length in one sliding-DFT launch).  Every symbol's
+    sampled windows -- both ends, a spread, and windows either side of the segment seams of every
+    segment length the launcher may pick -- against the oracle (1e-10 full row and in band); the
+    whole of every symbol's output against its own single-symbol plan (1e-10)."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    bars, lens = 20000, (512, 1024, 2048, 4096)
+    nwins = [bars - lens[s // 7] + 1 for s in range(28)]
+    series = [synth.random_walk_torch(bars, 100 + s, dev) for s in range(28)]
+    outs = [torch.full((nwins[s] * (lens[s // 7] // 2),), float("nan"), dtype=torch.float64, device=dev)
+            for s in range(28)]
+    g = bridge.Group(0, [lens[s // 7] for s in range(28)], nwins)
+    assert g.launches == 4
+    assert g.algorithmic_bytes == sum((bars + nwins[s] * (lens[s // 7] // 2)) * 8 for s in range(28))
+    g.execute([x.data_ptr() for x in series], [o.data_ptr() for o in outs], torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    worst = 0.0
+    rng = np.random.default_rng(8)
+    for s in range(28):
+        n, nw = lens[s // 7], nwins[s]
+        P = outs[s].view(nw, n // 2)
+        assert torch.isfinite(P).all().item()
+        seams = np.concatenate([[k * sg - 1, k * sg] for sg in (32, 64, 128, 256) for k in (1, nw // sg)])
+        idx = np.unique(np.clip(np.r_[0, 1, nw - 2, nw - 1, rng.integers(0, nw, 6), seams], 0, nw - 1))
+        x = series[s].cpu().numpy()
+        want = np.stack([oracle.window_spectrum(x[i:i + n], "none", "hann") for i in idx])
+        got = P[torch.from_numpy(idx).to(dev)].cpu().numpy()
+        assert oracle.rel_err(got, want) <= 1e-10, s
+        assert oracle.inband_err(got, want, *oracle.band(n)) <= 1e-10, s
+        worst = max(worst, oracle.rel_err(got, want))
+        plan = bridge.Plan(0, n, 1, nw, "none", "hann")
+        ref = torch.empty_like(outs[s])
+        plan.execute(series[s].data_ptr(), ref.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        Q = ref.view(nw, n // 2)
+        rel = ((P - Q).abs().amax(dim=1) / Q.abs().amax(dim=1)).max().item()
+        assert rel <= 1e-10, (s, rel)
+        plan.close()
+    _record("c5_group", symbols=28, rel_err=worst)
+    g.close()

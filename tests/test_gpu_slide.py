@@ -224,10 +224,11 @@ def test_slide_topk_matches_oracle(gpu_session, n, window, detrend):
 
 
 @pytest.mark.parametrize("k,pmin,pmax", [(1, 18.0, 200.0), (64, 18.0, 200.0), (8, 4.0, 2000.0), (8, 100.0, 110.0),
-                                         (8, 4.1, 9.0)])
+                                         (8, 4.1, 9.0), (8, 9.0, 30.0), (3, 18.0, 200.0), (8, 7.5, 30.0)])
 def test_slide_topk_slots_and_bands(gpu_session, k, pmin, pmax):
-    """k = 1 and 64 slots, bands of 512 / 1-2 / ~250 bins (one to eight bins per lane), empty slots when
-    the band holds fewer bins than k; segments of 100 windows (ragged seams)."""
+    """k = 1, 3, 8 and 64 slots, bands of 510 / 272 / 256 / 159 / 103 / 2 bins (one to eight bins per lane: the
+    transposed lane-per-window scan up to 256 bins and k <= 8, the one-wave scan beyond), empty slots when
+    the band holds fewer bins than k; segments of 100 windows (ragged seams, partial staged batches)."""
     torch = pytest.importorskip("torch")
     n, nwin = 2048, 1000
     s = synth.random_walk(nwin + n - 1, seed=k)
@@ -344,3 +345,44 @@ def test_stateful_plan_on_two_streams(gpu_session, kind):
     for i in range(2):
         assert torch.equal(outs[i], alone[i]), (kind, i)
     plan.close()
+
+
+@pytest.mark.parametrize("prec,detrend,window", [("f64", "none", "hann"), ("f64", "mean", "blackman"),
+                                                 ("f32", "mean", "hamming"), ("f64", "none", "none")])
+def test_group_mixed_members(gpu_session, prec, detrend, window):
+    """Grouped hop = 1 plan (wsp_group_*) with mixed window lengths, more than 16 members of one length
+    (two launches for it), a one-window member and members shorter than a segment: every window of every
+    member against the oracle."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    lens = [512] * 18 + [1024, 2048, 4096, 1024, 512]
+    nwins = [40 + 37 * i for i in range(18)] + [300, 1, 700, 5, 33]
+    tdt = torch.float32 if prec == "f32" else torch.float64
+    hs = [synth.random_walk(nw + n - 1, seed=200 + i) for i, (n, nw) in enumerate(zip(lens, nwins))]
+    series = [torch.from_numpy(h).to(dev, tdt) for h in hs]
+    outs = [torch.empty(nw * (n // 2), dtype=tdt, device=dev) for n, nw in zip(lens, nwins)]
+    g = bridge.Group(0, lens, nwins, detrend, window, prec)
+    assert g.launches == 2 + 3  # 512: 19 members in two launches; 1024, 2048, 4096 one each
+    g.execute([x.data_ptr() for x in series], [o.data_ptr() for o in outs], torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    tol = 1e-5 if prec == "f32" else 1e-10
+    for i, (n, nw) in enumerate(zip(lens, nwins)):
+        got = outs[i].double().cpu().numpy().reshape(nw, n // 2)
+        h = hs[i].astype(np.float32).astype(np.float64) if prec == "f32" else hs[i]
+        want = oracle.batch_spectrum(h, n, 1, detrend, window)
+        assert oracle.rel_err(got, want) <= tol, (i, n, nw)
+    g.close()
+
+
+def test_group_refusals(gpu_session):
+    """Members the sliding DFT cannot take are refused at creation (no silent fallback)."""
+    with pytest.raises(bridge.BridgeError):
+        bridge.Group(0, [256], [100])  # N below 512
+    with pytest.raises(bridge.BridgeError):
+        bridge.Group(0, [1024], [100], window="bartlett")  # not a cosine sum
+    with pytest.raises(bridge.BridgeError):
+        bridge.Group(0, [1024], [100], detrend="kalman")
+    with pytest.raises(bridge.BridgeError):
+        bridge.Group(0, [8192], [100], window="blackman")
+    with pytest.raises(ValueError):
+        bridge.Group(0, [1024, 512], [100])
