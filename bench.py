@@ -64,9 +64,11 @@ def parse(argv=None):
     ap.add_argument("--algo", default="auto", choices=["auto", "fft", "slide"],
                     help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
     ap.add_argument("--slide-seg", type=int, default=0, help="windows per sliding-DFT workgroup (0 = library policy)")
+    ap.add_argument("--variant", type=int, default=0, help="kernel form (wsp_plan_set_variant; ablations)")
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
                     help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
-    ap.add_argument("--c5-streams", type=int, default=3, help="C5: streams the symbol plans are spread over")
+    ap.add_argument("--c5-streams", type=int, default=1,
+                    help="C5: streams the grouped plan forks over (wsp_group_set_streams) / the symbol plans use")
     ap.add_argument("--c5-mode", default="group", choices=["group", "plans"],
                     help="C5: one grouped device plan (wsp_group_*: one launch per window length) or one plan per "
                          "symbol spread over --c5-streams streams (round-2 form, ablation)")
@@ -289,7 +291,7 @@ def shard_plan(name: str, rank: int, world: int, scaling: str) -> dict:
 class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
-    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0):
+    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -321,6 +323,8 @@ class SingleBatch(Workload):
                 self.plan.set_algorithm(algo)
             if slide_seg:
                 self.plan.set_slide_segment(slide_seg)
+            if variant:
+                self.plan.set_variant(variant)
         self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
         del full
         self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
@@ -371,14 +375,19 @@ class C5Batch(Workload):
         self.group = None
         self.describe = (f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2"
                          + (f", {len(owned)} symbols on this rank" if scaling == "strong" else ""))
-        if c5_mode == "group" and algo in ("auto", "slide") and not slide_seg:
+        if c5_mode == "group" and algo in ("auto", "slide"):
             self.series = [synth.random_walk_torch(bars, 100 + sym + seed_off, dev) for sym in owned]
             self.outs = [torch.empty(nwins[sym] * (lens[sym // 7] // 2), dtype=torch.float64, device=dev)
                          for sym in owned]
             self.group = bridge.Group(local_rank, [lens[sym // 7] for sym in owned], [nwins[sym] for sym in owned])
+            if c5_streams != 1:
+                self.group.set_streams(c5_streams)
+            if slide_seg:
+                self.group.set_segment(slide_seg)
             self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
             self.algorithm = "slide-group"
-            self.layout = {"mode": "group", "launches": self.group.launches}
+            self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams,
+                           "segment": slide_seg or "auto"}
             self.windows = sum(nwins[sym] for sym in owned)
             self.alg_bytes = self.group.algorithmic_bytes
             self.traffic = load_traffic("c5")
@@ -479,7 +488,7 @@ def main(argv=None):
         wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.c5_layout, args.c5_streams,
                      args.c5_mode)
     else:
-        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg)
+        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.variant)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)

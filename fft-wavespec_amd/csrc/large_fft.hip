@@ -310,6 +310,184 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
     }
 }
 
+// ---------------------------------------------------------------- fused form
+// One workgroup per window at a time (persistent: workgroup g takes windows g, g + grid, ...): the
+// column pass and the row pass of the same window back to back, the column results Y in a slot of
+// the workgroup's own (M complex) that the next window reuses.  With one workgroup per CU the slots
+// in flight are 256 x 512 KiB = 128 MiB at N = 65536, inside the 256 MiB Infinity Cache, so the Y round
+// trip is served from cache instead of HBM (two-pass form: the whole chunk's Y goes through HBM, PMC
+// 2.38x the algorithmic bytes).  The probe that priced this (tools/mall_probe.hip,
+// profiles/r02/large_slot_probe.log): the algorithmic bytes alone 620-665 us, + ~330 us for the
+// recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
+// post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
+// (workgroup-scope release / acquire; one CU, one L1).
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED>
+__global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
+    using GC = LGeo<LOG2M2>;
+    using GR = LGeo<LOG2M1>;
+    constexpr int RB = RowGeo<LOG2M1>::RB;
+    constexpr int M1 = GR::L, M2 = GC::L, TPC = GC::TP, TPR = GR::TP, NB1 = M1 / kCB, NB2 = (M2 / 2) / RB;
+    static_assert(kCB * TPC == 256 && 2 * RB * TPR == 256, "256 threads in both passes");
+    constexpr int64_t M = (int64_t)M1 * M2;
+    constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
+    constexpr int LDS_C = kCB * GC::SLOT, LDS_R = 2 * RB * GR::SLOT;
+    __shared__ cpx<T> lds[LDS_C > LDS_R ? LDS_C : LDS_R];
+    const int tid = threadIdx.x;
+    const T *__restrict__ series = static_cast<const T *>(a.series);
+    const cpx<T> *__restrict__ tw = static_cast<const cpx<T> *>(a.tw);
+    cpx<T> *__restrict__ y = static_cast<cpx<T> *>(a.y) + (int64_t)blockIdx.x * M;  // this workgroup's slot
+    const int N = 1 << a.log2n;
+    using v2 = typename core::V2<T>::t;
+    // column pass geometry (col_kernel): column c of the block, transform thread t
+    const int cc = tid % kCB, ct = tid / kCB;
+    // row pass geometry (row_kernel): slot rho, transform thread t
+    const int rho = tid / TPR, rt = tid % TPR;
+    v2 raw[16];
+    auto load_cols = [&](int64_t w, int beta) {  // 16 sample pairs of column beta * kCB + cc
+        const T *__restrict__ xw = series + w * a.hop;
+        const int n1 = beta * kCB + cc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = n1 + M1 * (ct + TPC * r);
+            if (a.vec) {
+                raw[r] = __builtin_nontemporal_load(reinterpret_cast<const v2 *>(xw + 2 * n));
+            } else {
+                raw[r].x = xw[2 * n];
+                raw[r].y = xw[2 * n + 1];
+            }
+        }
+    };
+    cpx<T> nxt[16];
+    auto load_rows = [&](int beta2) {
+        const int i = rho < RB ? rho : rho - RB, lo = beta2 * RB + i;
+        const int row = rho < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
+        const cpx<T> *__restrict__ yr = y + (int64_t)row * M1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[r] = yr[rt + TPR * r];
+    };
+    int64_t w = blockIdx.x;
+    if (w < a.nwin) load_cols(w, 0);
+    for (; w < a.nwin; w += gridDim.x) {
+        // ---- column pass: NB1 blocks of kCB columns
+        const double mean = MEAN ? a.means[w] : 0.0;
+        for (int beta = 0; beta < NB1; ++beta) {
+            const int n1 = beta * kCB + cc;
+            double cw = 1.0, sw = 0.0;
+            if constexpr (kCos) sincos(a.inv_theta * (double)(2 * (n1 + M1 * ct)), &sw, &cw);
+            int nb = n1 + M1 * ct;
+            if constexpr (WCLASS == core::kWinBartlett) asm volatile("" : "+v"(nb));
+            cpx<T> v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = nb + M1 * TPC * r;
+                double xa = (double)raw[r].x, xb = (double)raw[r].y;
+                if constexpr (MEAN) {
+                    xa -= mean;
+                    xb -= mean;
+                }
+                if constexpr (kCos) {
+                    const double co = cw * a.c1 - sw * a.s1;
+                    if constexpr (WCLASS == core::kWinCos2) {
+                        xa *= a.a0 + a.a1 * cw + a.a2 * (2.0 * cw * cw - 1.0);
+                        xb *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                    } else {
+                        xa *= a.a0 + a.a1 * cw;
+                        xb *= a.a0 + a.a1 * co;
+                    }
+                    const double cn = cw * a.cd - sw * a.sd;
+                    sw = sw * a.cd + cw * a.sd;
+                    cw = cn;
+                } else if constexpr (WCLASS == core::kWinBartlett) {  // L/WaveSpecZZ_1.0.2.mq5:918-922
+                    xa *= 1.0 - fabs((2.0 * (2 * n) - N + 1) * a.inv_nm1);
+                    xb *= 1.0 - fabs((2.0 * (2 * n + 1) - N + 1) * a.inv_nm1);
+                }
+                v[r] = {(T)xa, (T)xb};
+            }
+            // next block's samples (or the next window's first block) in flight during this FFT
+            if (beta + 1 < NB1) load_cols(w, beta + 1);
+            else if (w + gridDim.x < a.nwin) load_cols(w + gridDim.x, 0);
+            wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
+            constexpr int R = last_radix<LOG2M2>();
+            const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
+#pragma unroll
+            for (int q = 0; q < 16 / R; ++q) {
+                cpx<T> wr = tw[(2 * n1 * (ct + TPC * q)) & (N - 1)];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k2 = ct + TPC * q + (M2 / R) * r;
+                    y[(int64_t)k2 * M1 + n1] = cmul(v[q * R + r], wr);
+                    if (r + 1 < R) wr = cmul(wr, wstep_r);
+                }
+            }
+        }
+        __syncthreads();  // Y of this window complete and visible to the workgroup
+        // ---- row pass: NB2 blocks of RB rows + their mirror rows
+        load_rows(0);
+        for (int beta2 = 0; beta2 < NB2; ++beta2) {
+            const int i = rho < RB ? rho : rho - RB, lo = beta2 * RB + i;
+            const int row = rho < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
+            cpx<T> *slot = lds + rho * GR::SLOT;
+            cpx<T> v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = nxt[r];
+            if (beta2 + 1 < NB2) load_rows(beta2 + 1);
+            wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
+            constexpr int R = last_radix<LOG2M1>();
+#pragma unroll
+            for (int q = 0; q < 16 / R; ++q)
+#pragma unroll
+                for (int r = 0; r < R; ++r) slot[pad16(rt + TPR * q + (M1 / R) * r)] = v[q * R + r];
+            __syncthreads();
+            const bool self = row == 0 || row == M2 / 2;
+            const cpx<T> *pslot = lds + (self ? rho : (rho < RB ? rho + RB : rho - RB)) * GR::SLOT;
+            T res[16][PACKED ? 2 : 1];
+            const cpx<T> wstep_r = tw[(M2 * (M1 / R)) & (N - 1)];
+#pragma unroll
+            for (int q = 0; q < 16 / R; ++q) {
+                cpx<T> wk = tw[(row + M2 * (rt + TPR * q)) & (N - 1)];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k1 = rt + TPR * q + (M1 / R) * r;
+                    const int pk1 = row == 0 ? ((M1 - k1) & (M1 - 1)) : (M1 - 1 - k1);
+                    const cpx<T> z = v[q * R + r], zp = cconj(pslot[pad16(pk1)]);
+                    const cpx<T> e = {T(0.5) * (z.re + zp.re), T(0.5) * (z.im + zp.im)};
+                    const cpx<T> d = {T(0.5) * (z.re - zp.re), T(0.5) * (z.im - zp.im)};
+                    const cpx<T> o = {d.im, -d.re};
+                    const cpx<T> x = cadd(e, cmul(wk, o));
+                    if (r + 1 < R) wk = cmul(wk, wstep_r);
+                    if constexpr (PACKED) {
+                        res[q * R + r][0] = x.re;
+                        res[q * R + r][1] = x.im;
+                    } else {
+                        res[q * R + r][0] = x.re * x.re + x.im * x.im;
+                    }
+                }
+            }
+            __syncthreads();
+            constexpr int E = PACKED ? 2 : 1;
+            T *stage = reinterpret_cast<T *>(lds);
+#pragma unroll
+            for (int q = 0; q < 16 / R; ++q)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k1 = rt + TPR * q + (M1 / R) * r;
+#pragma unroll
+                    for (int e = 0; e < E; ++e) stage[(k1 * (2 * RB + 1) + rho) * E + e] = res[q * R + r][e];
+                }
+            __syncthreads();
+            T *__restrict__ ow = static_cast<T *>(ra.out) + w * (int64_t)(PACKED ? 2 * M : M);
+            for (int ii = tid; ii < M1 * 2 * RB; ii += 256) {
+                const int sl = ii % (2 * RB), k1 = ii / (2 * RB);
+                const int il = sl < RB ? sl : sl - RB, l2 = beta2 * RB + il;
+                const int64_t k = (sl < RB ? l2 : (l2 == 0 ? M2 / 2 : M2 - l2)) + (int64_t)M2 * k1;
+#pragma unroll
+                for (int e = 0; e < E; ++e) ow[k * E + e] = stage[(k1 * (2 * RB + 1) + sl) * E + e];
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // ---------------------------------------------------------------- pre-passes
 
 // Per-window mean (L/WaveSpecZZ_gpu_wip.mq5:940-950) for the column pass.
@@ -447,6 +625,37 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
     return L.packed ? row_launch<T, LM1, LM2, true>(ra, s) : row_launch<T, LM1, LM2, false>(ra, s);
 }
 
+// the fused form for M2 = 256 (N = 65536, 131072): one launch over every window
+template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0,
+                                                       const large::RowArgs &ra, int wclass, bool mean, hipStream_t s) {
+    large::ColArgs ca = ca0;
+    ca.w0 = 0;
+    ca.nwin = L.n_windows;
+    // workgroups in flight: one per CU by default (slots stay in the Infinity Cache), two with variant 3;
+    // never more slots than the plan workspace holds (a chunk of windows)
+    const int per_cu = L.variant == 3 ? 2 : 1;
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>({L.n_windows, L.chunk, (int64_t)per_cu * cu_count()}));
+    hipError_t e = hipSuccess;
+    using namespace core;
+#define FUSED(WC)                                                                                                          \
+    if (mean) {                                                                                                            \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+    } else {                                                                                                               \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+    }
+    switch (wclass) {
+    case kWinCos: FUSED(kWinCos); break;
+    case kWinCos2: FUSED(kWinCos2); break;
+    case kWinBartlett: FUSED(kWinBartlett); break;
+    default: FUSED(kWinNone); break;
+    }
+#undef FUSED
+    e = hipGetLastError();
+    return e;
+}
+
 template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     const int log2m = L.log2n - 1;
     const int n = 1 << L.log2n;
@@ -499,6 +708,13 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     ra.tw = L.twiddle;
     ra.log2n = L.log2n;
     ra.packed = L.packed;
+    ra.w0 = 0;
+    ra.nwin = L.n_windows;
+    // fused form (one launch, Y through the Infinity Cache) for N = 65536 / 131072; variant 1 forces the
+    // two-pass form (ablation)
+    if (L.variant != 1 && (log2m == 15 || log2m == 16))
+        return log2m == 15 ? fused_launch<T, 7>(L, ca, ra, wclass, means != nullptr, s)
+                           : fused_launch<T, 8>(L, ca, ra, wclass, means != nullptr, s);
     for (int64_t w0 = 0; w0 < L.n_windows; w0 += L.chunk) {
         ca.w0 = ra.w0 = w0;
         ca.nwin = ra.nwin = std::min<int64_t>(L.chunk, L.n_windows - w0);

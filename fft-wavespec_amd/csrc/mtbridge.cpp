@@ -293,6 +293,11 @@ int get_slide_table(int dev, int log2n, int window, void **out) {
     return MTB_OK;
 }
 
+// Longest sliding-DFT segment a caller may ask for: a tracker's rounding grows linearly with the
+// number of slides (sliding_dft.hip), and parity is tested up to this length
+// (tests/test_gpu_slide.py::test_slide_vs_fft_large_segments).
+constexpr int64_t kSlideMaxSegment = 2048;
+
 // ----------------------------------------------------------------- config
 enum Op : int { kOpSpectrum = 0, kOpInverse = 1 };
 struct Config {
@@ -303,6 +308,7 @@ struct Config {
     int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK / MTB_OUT_TOPK_PHASE
     int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
     int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
+    int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
     int64_t record() const {
@@ -531,6 +537,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         G.window = c.window;
         G.packed = c.output == MTB_OUT_PACKED;
         G.f32 = c.f32;
+        G.variant = c.variant;
         HIP_OR(launch_large(G, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
@@ -543,6 +550,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         A.n_windows = c.n_windows;
         if (topk) {
             A.seg = slide_topk_seg(c);
+            A.variant = c.variant;
             A.kmin = c.kmin;
             A.span = c.kmax - c.kmin + 1;
             A.topk = c.topk;
@@ -1073,6 +1081,24 @@ struct Group {
     int dev = 0;
     std::vector<Config> cfg;               // one per member (hop 1, power)
     std::vector<std::vector<int>> launch;  // member indices per launch: one window length, <= kSlideGroupMax
+    std::vector<int64_t> launch_bytes;     // output bytes per launch: what the slide's time follows
+    std::mutex mu;                         // executes on the internal streams are enqueued one at a time
+    int64_t seg = 0;                       // windows per workgroup, 0 = the launcher's policy
+    // wsp_group_set_streams(n > 1): the launches fork from the caller's stream onto n internal streams
+    // (greedy by output bytes, longest first) and join back, so that one length's tail overlaps the next
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;  // [0] fork, [1 + i] join of stream i
+    void release() {
+        (void)hipSetDevice(dev);
+        for (auto st : streams) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+        for (auto e : events) (void)hipEventDestroy(e);
+        streams.clear();
+        events.clear();
+    }
+    ~Group() { release(); }
 };
 std::mutex g_groups_mu;
 std::map<int64_t, std::shared_ptr<Group>> *g_groups = new std::map<int64_t, std::shared_ptr<Group>>();
@@ -1665,10 +1691,17 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
     return sw;
 }
 
-// Longest sliding-DFT segment a caller may ask for: a tracker's rounding grows linearly with the
-// number of slides (sliding_dft.hip), and parity is tested up to this length
-// (tests/test_gpu_slide.py::test_slide_vs_fft_large_segments).
-constexpr int64_t kSlideMaxSegment = 2048;
+MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || variant < 0 || variant > 3) {
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..3", (long long)plan, variant);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.variant = variant;
+    return MTB_OK;
+}
+
 
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
     std::shared_ptr<Plan> p = find_plan(plan);
@@ -1743,9 +1776,13 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
         by_len[c.n].push_back(m);
     }
     for (auto &kv : by_len)
-        for (size_t i = 0; i < kv.second.size(); i += kSlideGroupMax)
+        for (size_t i = 0; i < kv.second.size(); i += kSlideGroupMax) {
             g->launch.emplace_back(kv.second.begin() + i,
                                    kv.second.begin() + std::min(kv.second.size(), i + (size_t)kSlideGroupMax));
+            int64_t b = 0;
+            for (int m : g->launch.back()) b += g->cfg[m].n_windows * g->cfg[m].record() * (int64_t)g->cfg[m].elem();
+            g->launch_bytes.push_back(b);
+        }
     const int64_t id = g_next_id.fetch_add(1);
     std::lock_guard<std::mutex> lk(g_groups_mu);
     (*g_groups)[id] = std::move(g);
@@ -1767,10 +1804,21 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
             set_error("wsp_group_execute: member %zu has a null device buffer", m);
             return MTB_BAD_ARGS;
         }
-    for (const auto &L : g->launch) {
+    std::lock_guard<std::mutex> lk(g->mu);
+    const hipStream_t caller = (hipStream_t)hip_stream;
+    const int ns = (int)g->streams.size();
+    HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
+    if (ns > 1) {
+        HIP_OR(hipEventRecord(g->events[0], caller), MTB_INTERNAL_ERROR);
+        for (auto st : g->streams) HIP_OR(hipStreamWaitEvent(st, g->events[0], 0), MTB_INTERNAL_ERROR);
+    }
+    std::vector<int64_t> load(ns > 1 ? ns : 1, 0);
+    for (size_t li = 0; li < g->launch.size(); ++li) {  // longest windows first; greedy by output bytes
+        const auto &L = g->launch[li];
         SlideArgs A{};
         const int st = slide_args(g->dev, g->cfg[L[0]], &A);
         if (st != MTB_OK) return st;
+        A.seg = g->seg;
         SlideGroup G;
         G.n = (int)L.size();
         for (int i = 0; i < G.n; ++i) {
@@ -1778,8 +1826,58 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
             G.out[i] = d_out[L[i]];
             G.n_windows[i] = g->cfg[L[i]].n_windows;
         }
-        HIP_OR(launch_slide_group(A, G, (hipStream_t)hip_stream), MTB_INTERNAL_ERROR);
+        const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[k] += g->launch_bytes[li];
+        HIP_OR(launch_slide_group(A, G, ns > 1 ? g->streams[k] : caller), MTB_INTERNAL_ERROR);
     }
+    if (ns > 1)
+        for (int i = 0; i < ns; ++i) {
+            HIP_OR(hipEventRecord(g->events[1 + i], g->streams[i]), MTB_INTERNAL_ERROR);
+            HIP_OR(hipStreamWaitEvent(caller, g->events[1 + i], 0), MTB_INTERNAL_ERROR);
+        }
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g || n_streams < 1 || n_streams > 8) {
+        set_error("wsp_group_set_streams(%lld, %d): unknown group or n_streams outside 1..8", (long long)group, n_streams);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->release();
+    if (n_streams == 1) return MTB_OK;
+    HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
+    for (int i = 0; i < n_streams; ++i) {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+            g->release();
+            set_error("wsp_group_set_streams: stream creation failed");
+            return MTB_INTERNAL_ERROR;
+        }
+        g->streams.push_back(st);
+    }
+    for (int i = 0; i <= n_streams; ++i) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            g->release();
+            set_error("wsp_group_set_streams: event creation failed");
+            return MTB_INTERNAL_ERROR;
+        }
+        g->events.push_back(e);
+    }
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g || windows < 0 || windows > kSlideMaxSegment) {
+        set_error("wsp_group_set_segment(%lld, %lld): unknown group or length outside 0..%lld", (long long)group,
+                  (long long)windows, (long long)kSlideMaxSegment);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->seg = windows;
     return MTB_OK;
 }
 

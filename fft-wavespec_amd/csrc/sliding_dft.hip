@@ -1,654 +1,9 @@
-// sliding_dft.hip -- hop = 1 batches by a seeded sliding DFT (gfx950).
-//
-// The same quantity as spectrum_kernel -- per window w: x[w .. w+N) -> [mean detrend] -> cosine
-// window (L/WaveSpecZZ_1.0.2.mq5:884-922) -> DFT (FourierTransformManual, :938-974) -> |X_k|^2,
-// k < N/2 (1.1.0:529-530) -- for consecutive windows (hop = 1 bar, the batch-warmup and
-// fetcher shape: 1.1.0:1014-1020, WaveCyclesBatchFetcher.mq5:106-133), computed by a different
-// exact-in-real-arithmetic route that does ~2.5x less fp64 work per window than an FFT.
-//
-// With the window a0 + a1 cos(th i) + a2 cos(2 th i), th = 2 pi/(N-1), and
-// S_w(f) = sum_i x[w+i] e^{-2 pi j f i}:
-//     X_w[k] = a0 S_w(k/N) + a1/2 (S_w(k/N + phi) + S_w(k/N - phi)) + a2/2 (S_w(k/N +- 2 phi)),
-//     phi = 1/(N-1).
-// Each S slides by one sample exactly:
-//     S_{w+1}(f) = e^{2 pi j f} (S_w(f) - x[w] + x[w+N] e^{-2 pi j f N}),
-// and for f = k/N + m phi the factor e^{-2 pi j f N} = e^{-j m th} is the same for every bin, so
-// one step of one tracker T_f = s_f S_f is T <- omega_f (T + u_m) with a per-step uniform u_m:
-// 5-6 fp64 operations per tracker, 23 per bin and window for Hann (|X|^2 included) against
-// ~57 for the radix-16/8 FFT at N = 2048.  The mean detrend is linear:
-// X_w - mean_w * H[k], H = DFT of the window.
-//
-// Layout: one workgroup per segment of consecutive windows (32..256 windows, about two rounds of
-// resident workgroups: launch_t), N/(2B) threads; thread t owns bins k = 2 (t + NT q) + e (q < B/2,
-// e < 2), so every store instruction of a wave writes 128 consecutive bins (1 KiB fp64) as one 16-B
-// store per lane.  The segment's trackers are SEEDED exactly, not slid from the previous segment:
-// Y_m = FFT_N(x[w0 + i] e^{-j m th i}) in LDS (radix-4 Stockham, quarter twiddle table in LDS) gives
-// S(k/N + m phi) = Y_m[k] and S(k/N - m phi) = conj(Y_m[N-k]).  The per-step uniforms
-// (u_0, u_1, u_2, x[w+N] - x[w]) are staged in LDS a chunk at a time and read by broadcast.
-// With the mean detrend the trackers follow the samples minus the segment's first sample.
-// Rounding: a tracker's error grows at most linearly with the segment length (<= 256 steps by
-// default: ~3e-14 of its own magnitude); the parity bars are BASELINE.md 2's (tests/test_gpu_slide.py,
-// tests/test_gpu_fullgrid.py, the CPU model tests/test_slide_model.py).
-//
-// Top-k records (MTB_OUT_TOPK, fp64) at hop = 1 track only the scan band's bins: slide_seed_kernel writes every
-// segment's band trackers to the plan workspace, slide_topk_kernel slides them one wave per segment and runs the FFT
-// kernel's one-wave scan (core::topk_wave64) on each window's band, staged in LDS.
-#include <atomic>
-
-#include "spectrum_core.h"  // topk_wave64: the one-wave top-k scan of the FFT kernel
-#include "wsp_internal.h"
+// sliding_dft.hip -- hop = 1 batches by a seeded sliding DFT (gfx950): the library's entry points
+// (power rows of one series or of a group of series, top-k records) and the fp64 power kernels.
+// Device code and design notes: sliding_core.h.
+#include "sliding_core.h"
 
 namespace wsp {
-namespace {
-
-typedef double d2 __attribute__((ext_vector_type(2)));
-
-// bins per thread: 4, or 2 for windows up to 1024 (C5's short-window plans: twice the threads per
-// workgroup for the same segment)
-template <int LOG2N> constexpr int slide_b() { return LOG2N <= 10 ? 2 : 4; }
-constexpr int kSlideRMax = 512;  // most steps whose uniforms are staged in LDS at once
-
-template <int NF> struct Rec { static constexpr int n = NF + 1; };  // [u0, (u1r, u1i), (u2r, u2i), d]
-
-__device__ __forceinline__ d2 cmul(d2 a, d2 b) { return d2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
-
-// In-place natural-order complex FFT of N points in LDS: Stockham DIT, one radix-2 stage first when
-// log2 N is odd, then radix 4; NT threads.  twl[k] = W_N^k for k < N/4 (LDS, or the global table at
-// N = 8192 where LDS is full); a radix-4 butterfly loads W^k and forms W^2k, W^3k by products.
-// Ends after a barrier.
-template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, const d2 *twl) {
-    constexpr int N = 1 << LOG2N, H = N / 2, N4 = N / 4;
-    const int t = threadIdx.x;
-    int ns = 1;
-    if constexpr (LOG2N & 1) {  // radix 2, Ns = 1: no twiddles
-        constexpr int Q = H / NT;
-        d2 a[Q], b[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            a[q] = buf[t + NT * q];
-            b[q] = buf[t + NT * q + H];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int j = t + NT * q;
-            buf[2 * j] = a[q] + b[q];
-            buf[2 * j + 1] = a[q] - b[q];
-        }
-        __syncthreads();
-        ns = 2;
-    }
-    constexpr int Q = N4 / NT;
-#pragma unroll 1
-    for (; ns < N; ns *= 4) {
-        const int tws = N / (4 * ns);  // W_{4 Ns}^k = W_N^{k N/(4 Ns)}
-        d2 v[Q][4], w1[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int j = t + NT * q;
-            w1[q] = twl[(j & (ns - 1)) * tws];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * N4];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int j = t + NT * q, k = j & (ns - 1);
-            const d2 w2 = cmul(w1[q], w1[q]), w3 = cmul(w1[q], w2);
-            const d2 x1 = cmul(v[q][1], w1[q]), x2 = cmul(v[q][2], w2), x3 = cmul(v[q][3], w3);
-            const d2 t0 = v[q][0] + x2, t1 = v[q][0] - x2, t2 = x1 + x3, d = x1 - x3;
-            const d2 t3 = d2{d.y, -d.x};  // -i (x1 - x3)
-            const int o = ((j - k) << 2) + k;
-            buf[o] = t0 + t2;
-            buf[o + ns] = t1 + t3;
-            buf[o + 2 * ns] = t0 - t2;
-            buf[o + 3 * ns] = t1 - t3;
-        }
-        __syncthreads();
-    }
-}
-
-// Bin b of thread t: pairs of adjacent bins, 2 (t + NT (b / 2)) + b % 2, so that a wave's store of a pair
-// of powers is one 16-B access per lane (1 KiB contiguous per wave instruction).
-template <int NT> __device__ __forceinline__ int kbin_of(int t, int b) { return 2 * (t + NT * (b >> 1)) + (b & 1); }
-
-// The segment's seeds: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}), m = 0 .. (NF-1)/2, in LDS; pick(m, s_m, Y)
-// takes what it needs from each transform (every thread calls it between the transform's barriers).
-template <typename T, int LOG2N, int NF, int DETREND, int NT, typename PICK>
-__device__ __forceinline__ void seed_ffts(const SlideArgs &a, const T *__restrict__ x, double lvl, d2 *lds, d2 *twq,
-                                          PICK pick) {
-    constexpr int N = 1 << LOG2N, M = N / 2, NM = (NF - 1) / 2;
-    constexpr bool TWL = N <= 4096;  // the quarter twiddle table fits LDS beside the FFT buffer
-    const int t = threadIdx.x;
-    const d2 *__restrict__ tw = static_cast<const d2 *>(a.twiddle);
-    const d2 *__restrict__ mod = static_cast<const d2 *>(a.omega) + (NF + 1) * M;  // [NM][N]
-    const d2 *twl = tw;
-    if constexpr (TWL) {
-        for (int i = t; i < N / 4; i += NT) twq[i] = tw[i];
-        twl = twq;
-    }
-#pragma unroll
-    for (int m = 0; m <= NM; ++m) {
-        for (int i = t; i < N; i += NT) {
-            const double xi = (double)x[i] - lvl;
-            lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
-        }
-        __syncthreads();
-        fft_lds<LOG2N, NT>(lds, twl);
-        pick(m, m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2), lds);
-        __syncthreads();
-    }
-}
-
-// Per-step uniforms of steps c0 .. c0 + clen - 1 into u[st * REC]: u_m = s_m (x[w+N] e^{-j m th} - x[w]),
-// d = x[w+N] - x[w] (samples minus the segment's level L); no step after the segment's last window.
-template <typename T, int NF, int N>
-__device__ __forceinline__ void stage_uniforms(const SlideArgs &a, const T *__restrict__ x, double lvl, int c0,
-                                               int clen, int len, double *u, int t, int nt) {
-    constexpr int REC = Rec<NF>::n;
-    for (int st = t; st < clen; st += nt) {
-        if (c0 + st + 1 >= len) break;
-        const double xw = (double)x[c0 + st] - lvl, xn = (double)x[c0 + st + N] - lvl;
-        double *r = u + st * REC;
-        r[0] = a.s0 * (xn - xw);
-        if constexpr (NF >= 3) {
-            r[1] = a.s1 * (xn * a.c1 - xw);
-            r[2] = -(a.s1 * (xn * a.sn1));
-        }
-        if constexpr (NF >= 5) {
-            r[3] = a.s2 * (xn * a.c2 - xw);
-            r[4] = -(a.s2 * (xn * a.sn2));
-        }
-        r[REC - 1] = xn - xw;
-    }
-}
-
-// One slide of B bins' trackers: T_f <- omega_f (T_f + u_m); the mean path's running sum of x - L.
-template <int B, int NF, int DETREND>
-__device__ __forceinline__ void slide_step(d2 (&tr)[B][NF], const d2 (&om)[B][NF], const double *r, double &sum) {
-    const double u0 = r[0];
-#pragma unroll
-    for (int b = 0; b < B; ++b) tr[b][0] = cmul(om[b][0], d2{tr[b][0].x + u0, tr[b][0].y});
-    if constexpr (NF >= 3) {
-        const double u1r = r[1], u1i = r[2];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            tr[b][1] = cmul(om[b][1], tr[b][1] + d2{u1r, u1i});
-            tr[b][2] = cmul(om[b][2], tr[b][2] + d2{u1r, -u1i});
-        }
-    }
-    if constexpr (NF >= 5) {
-        const double u2r = r[3], u2i = r[4];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            tr[b][3] = cmul(om[b][3], tr[b][3] + d2{u2r, u2i});
-            tr[b][4] = cmul(om[b][4], tr[b][4] + d2{u2r, -u2i});
-        }
-    }
-    if constexpr (DETREND == kDetrendMean) sum += r[Rec<NF>::n - 1];
-}
-
-// Workgroup -> (member, segment) of a grouped launch (SlideGroup): members own contiguous runs of
-// workgroups.  Unrolled selects over the kernel-argument table (uniform scalar loads, no dynamic
-// indexing of the argument struct).
-struct SlideSeg {
-    const void *series;
-    void *out;
-    int64_t w0, n_windows;
-};
-__device__ __forceinline__ SlideSeg slide_seg_of(const SlideGroup &g, int64_t seg) {
-    const int64_t b = blockIdx.x;
-    SlideSeg r{g.series[0], g.out[0], b * seg, g.n_windows[0]};
-#pragma unroll
-    for (int i = 1; i < kSlideGroupMax; ++i)
-        if (i < g.n && b >= g.blk0[i]) r = SlideSeg{g.series[i], g.out[i], (b - g.blk0[i]) * seg, g.n_windows[i]};
-    return r;
-}
-
-template <typename T, int LOG2N, int NF, int DETREND>
-__global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
-                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a,
-                                                                                                              SlideGroup g) {
-    constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B;
-    constexpr int REC = Rec<NF>::n;
-    const SlideSeg sg = slide_seg_of(g, a.seg);  // this workgroup's member (a single plan is a group of one)
-    if (sg.w0 >= sg.n_windows) return;
-    // per-step uniforms staged CH steps at a time: N/4 clamped to [128, 512], so that small windows keep
-    // 4 single-/two-wave workgroups per SIMD (LDS: FFT buffer + quarter twiddles + uniforms)
-    constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
-    constexpr int LDS2 = (N > CH * REC / 2) ? N : CH * REC / 2;
-    constexpr bool TWL = N <= 4096;  // the quarter twiddle table fits LDS beside the FFT buffer
-    __shared__ d2 lds[LDS2];
-    __shared__ d2 twq[TWL ? N / 4 : 1];
-
-    const int t = threadIdx.x;
-    auto kbin = [](int tt, int b) { return kbin_of<NT>(tt, b); };
-    const int len = (int)((sg.n_windows - sg.w0) < a.seg ? (sg.n_windows - sg.w0) : a.seg);
-    const T *__restrict__ x = static_cast<const T *>(sg.series) + sg.w0;  // the segment's first window
-    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);  // [NF][M]
-    const d2 *__restrict__ hwin = omega + NF * M;                      // [M]
-
-    d2 om[B][NF], tr[B][NF];
-    // mean detrend: the trackers follow x - L, L = the segment's first sample, and the output subtracts
-    // (mean - L) H_k: X_w - mean_w H = X(x - L) - (mean_w - L) H.  Centring keeps the ~N x price level
-    // out of the trackers near DC (20x smaller rounding at bins 0-2, tests/test_slide_model.py).
-    const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
-
-    double sum0 = 0.0;
-    seed_ffts<T, LOG2N, NF, DETREND, NT>(a, x, lvl, lds, twq, [&](int m, double s, const d2 *y) {
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int k = kbin(t, b);
-            if (m == 0) {
-                tr[b][0] = s * y[k];
-            } else {
-                const d2 yp = y[k], ym = y[(N - k) & (N - 1)];
-                tr[b][2 * m - 1] = s * yp;
-                tr[b][2 * m] = s * d2{ym.x, -ym.y};
-            }
-        }
-        if (DETREND == kDetrendMean && m == 0) sum0 = y[0].x;  // broadcast read: sum of x - L
-    });
-
-#pragma unroll
-    for (int b = 0; b < B; ++b)
-#pragma unroll
-        for (int f = 0; f < NF; ++f) om[b][f] = omega[f * M + kbin(t, b)];
-    d2 hk[B];
-    double sum = 0.0;
-    if constexpr (DETREND == kDetrendMean) {
-#pragma unroll
-        for (int b = 0; b < B; ++b) hk[b] = hwin[kbin(t, b)];
-        sum = sum0;
-    }
-
-    T *__restrict__ out = static_cast<T *>(sg.out) + sg.w0 * M + 2 * t;
-    double *u = reinterpret_cast<double *>(lds);
-    for (int c0 = 0; c0 < len; c0 += CH) {
-        const int clen = len - c0 < CH ? len - c0 : CH;
-        if (c0) __syncthreads();  // the previous chunk's reads are done
-        stage_uniforms<T, NF, N>(a, x, lvl, c0, clen, len, u, t, NT);
-        __syncthreads();
-
-        // ---- slide
-#pragma unroll 1
-        for (int st = 0; st < clen; ++st) {
-            double mw = 0.0;
-            if constexpr (DETREND == kDetrendMean) mw = sum * a.inv_n;
-            double p[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                d2 X = tr[b][0];
-#pragma unroll
-                for (int f = 1; f < NF; ++f) X += tr[b][f];
-                if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
-                p[b] = X.x * X.x + X.y * X.y;
-            }
-            // bins 2(t + NT q) and 2(t + NT q) + 1: one 16-B (fp64) / 8-B (fp32) store per pair; plain
-            // stores: a pure write stream runs at 5.75 TB/s plain vs 5.5 non-temporal
-            // (tools/write_probe.hip, profiles/r02/slide/write_probe.log)
-#pragma unroll
-            for (int q = 0; q < B / 2; ++q) {
-                typedef T v2t __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)p[2 * q], (T)p[2 * q + 1]};
-            }
-            out += M;
-            if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
-        }
-    }
-}
-
-// Workgroups: each slides a segment of consecutive windows (seeded once, per-step uniforms staged CH
-// steps at a time); segment length from the residency (occupancy API, once per instantiation).
-// ---- hop = 1 top-k records (MTB_OUT_TOPK): only the band's bins are tracked.
-// Seeds of every segment into the workspace: [NF][span] trackers of bins kmin .. kmin + span - 1, then
-// {sum of x - L (mean path), L}; one workgroup per segment, the same in-LDS FFTs as slide_kernel.
-// threads of the seed pass: N/4 (one radix-4 butterfly per thread and stage), at most 1024
-template <int LOG2N> constexpr int seed_nt() { return (1 << LOG2N) / 4 < 1024 ? (1 << LOG2N) / 4 : 1024; }
-
-template <typename T, int LOG2N, int NF, int DETREND>
-__global__ __launch_bounds__(seed_nt<LOG2N>()) void slide_seed_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, NT = seed_nt<LOG2N>();
-    constexpr bool TWL = N <= 4096;
-    __shared__ d2 lds[N];
-    __shared__ d2 twq[TWL ? N / 4 : 1];
-    const int t = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
-    if (w0 >= a.n_windows) return;
-    const T *__restrict__ x = static_cast<const T *>(a.series) + w0;
-    const double lvl = DETREND == kDetrendMean ? (double)x[0] : 0.0;
-    d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
-    const int span = a.span, kmin = a.kmin;
-    seed_ffts<T, LOG2N, NF, DETREND, NT>(a, x, lvl, lds, twq, [&](int m, double s, const d2 *y) {
-        for (int j = t; j < span; j += NT) {
-            const int k = kmin + j;
-            if (m == 0) {
-                ws[j] = s * y[k];
-            } else {
-                const d2 ym = y[(N - k) & (N - 1)];
-                ws[(2 * m - 1) * span + j] = s * y[k];
-                ws[(2 * m) * span + j] = s * d2{ym.x, -ym.y};
-            }
-        }
-        if (m == 0 && t == 0) ws[NF * span] = d2{y[0].x, lvl};
-    });
-}
-
-// One wave per segment: lane l tracks bins kmin + l + 64 b (b < NB), stages each window's band X in LDS
-// and runs the FFT kernel's one-wave scan (core::topk_wave64: power desc, bin asc, as the reference's
-// strict-'>' insertion, L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554), which writes the
-// window's record row.
-template <int LOG2N, int NF, int DETREND, int NB>
-__global__ __launch_bounds__(64) void slide_topk_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128;
-    __shared__ double u[CHT * REC];
-    __shared__ core::cpx<double> xb[64 * NB];
-    const int l = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
-    if (w0 >= a.n_windows) return;
-    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
-    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
-    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
-    const d2 *__restrict__ hwin = omega + NF * M;
-    const d2 *__restrict__ ws = static_cast<const d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
-    const int span = a.span, kmin = a.kmin;
-    d2 tr[NB][NF], om[NB][NF], hk[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int j = l + 64 * b;
-        const bool ok = j < span;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            tr[b][f] = ok ? ws[f * span + j] : d2{0.0, 0.0};
-            om[b][f] = ok ? omega[f * M + kmin + j] : d2{1.0, 0.0};
-        }
-        hk[b] = (DETREND == kDetrendMean && ok) ? hwin[kmin + j] : d2{0.0, 0.0};
-    }
-    const d2 sl = ws[NF * span];
-    double sum = sl.x;
-    const double lvl = sl.y;
-    double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
-    for (int c0 = 0; c0 < len; c0 += CHT) {
-        const int clen = len - c0 < CHT ? len - c0 : CHT;
-        if (c0) __syncthreads();
-        stage_uniforms<double, NF, N>(a, x, lvl, c0, clen, len, u, l, 64);
-        __syncthreads();
-#pragma unroll 1
-        for (int st = 0; st < clen; ++st) {
-            const double mw = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                d2 X = tr[b][0];
-#pragma unroll
-                for (int f = 1; f < NF; ++f) X += tr[b][f];
-                if constexpr (DETREND == kDetrendMean) X -= mw * hk[b];
-                xb[l + 64 * b] = core::cpx<double>{X.x, X.y};
-            }
-            __syncthreads();  // one wave: orders the band's LDS writes before the scan's reads
-            core::topk_wave64<NB, double>(xb, kmin, span, a.topk, l, rec, true);
-            __syncthreads();  // the scan's reads before the next window's writes
-            rec += 4 * a.topk;
-            if (c0 + st + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
-        }
-    }
-}
-
-// ---- the same records by a transposed scan (k <= 8): lane per window instead of a wave per window.
-// The wave slides its band's trackers as slide_topk_kernel does (lane l: bins kmin + l + 64 b) and
-// stages WB consecutive windows' band X in LDS ([window][bin], odd row stride: the scan's 16-byte
-// reads of 16 rows are conflict-free).  Then the lanes turn to the windows: lane l scans window
-// l % WB over the quarter (LPW = 64 / WB parts) l / WB of the band with the reference's 8-slot
-// insertion in registers (strict '>' against slots sorted by power: an equal power goes after the
-// earlier, lower bin -- L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554), and the
-// LPW partial lists of a window are merged across lanes (log2 LPW rounds: exchange with the partner
-// lane, keep the best 8 of the two by a bitonic merge under the key (power desc, bin asc)).  Every
-// lane of a window then holds its top 8; lane part q writes slots 2q, 2q + 1 (Re / Im from LDS).
-// Against one wave-wide max + ballot per slot and window (topk_wave64: 8 dependent reduction rounds
-// per window), the scan is ~90 independent VALU operations per window and lane group.
-constexpr int kTopkT = 8;  // slots of the transposed scan (the reference's top 8); larger k: slide_topk_kernel
-
-__device__ __forceinline__ bool kbetter(double pa, int ba, double pb, int bb) { return pa > pb || (pa == pb && ba < bb); }
-
-template <int LOG2N, int NF, int DETREND, int NB, int WB>
-__global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128, LPW = 64 / WB, K = kTopkT;
-    constexpr int SPMAX = (64 * NB) | 1;  // the widest band this NB serves, odd
-    constexpr int kEmpty = 0x7fffffff;    // bin of an empty slot: sorts after every real bin
-    __shared__ double u[CHT * REC];
-    __shared__ d2 xs[WB * SPMAX];
-    const int l = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
-    if (w0 >= a.n_windows) return;
-    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
-    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
-    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
-    const d2 *__restrict__ hwin = omega + NF * M;
-    const d2 *__restrict__ ws = static_cast<const d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
-    const int span = a.span, kmin = a.kmin, sp = span | 1;
-    d2 tr[NB][NF], om[NB][NF], hk[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int j = l + 64 * b;
-        const bool ok = j < span;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            tr[b][f] = ok ? ws[f * span + j] : d2{0.0, 0.0};
-            om[b][f] = ok ? omega[f * M + kmin + j] : d2{1.0, 0.0};
-        }
-        hk[b] = (DETREND == kDetrendMean && ok) ? hwin[kmin + j] : d2{0.0, 0.0};
-    }
-    const d2 sl = ws[NF * span];
-    double sum = sl.x;
-    const double lvl = sl.y;
-    // the scan's lane roles: window mw of the staged batch, band part mq: bins [q0, q1)
-    const int mw = l % WB, mq = l / WB;
-    const int qs = (span + LPW - 1) / LPW, q0 = mq * qs, q1 = q0 + qs < span ? q0 + qs : span;
-    double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
-    const int kk = a.topk;
-    for (int c0 = 0; c0 < len; c0 += CHT) {
-        const int clen = len - c0 < CHT ? len - c0 : CHT;
-        if (c0) __syncthreads();
-        stage_uniforms<double, NF, N>(a, x, lvl, c0, clen, len, u, l, 64);
-        __syncthreads();
-#pragma unroll 1
-        for (int st = 0; st < clen; ++st) {
-            const int wi = c0 + st, slot = wi % WB;
-            const double mwv = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                d2 X = tr[b][0];
-#pragma unroll
-                for (int f = 1; f < NF; ++f) X += tr[b][f];
-                if constexpr (DETREND == kDetrendMean) X -= mwv * hk[b];
-                const int j = l + 64 * b;
-                if (j < span) xs[slot * sp + j] = X;
-            }
-            if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
-            if (slot != WB - 1 && wi + 1 < len) continue;
-            // ---- scan the staged batch: windows wi - slot .. wi
-            __syncthreads();
-            double tp[K];
-            int tb[K];
-#pragma unroll
-            for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
-            const bool wok = mw <= slot;
-            if (wok) {
-                const d2 *row = xs + mw * sp;
-                for (int j = q0; j < q1; ++j) {
-                    const d2 X = row[j];
-                    const double p = X.x * X.x + X.y * X.y;
-                    // insertion as the reference: first slot s with p > tp[s] takes it, the rest shift down
-                    bool c[K];
-#pragma unroll
-                    for (int s = 0; s < K; ++s) c[s] = p > tp[s];
-#pragma unroll
-                    for (int s = K - 1; s > 0; --s) {
-                        tp[s] = c[s] ? (c[s - 1] ? tp[s - 1] : p) : tp[s];
-                        tb[s] = c[s] ? (c[s - 1] ? tb[s - 1] : j) : tb[s];
-                    }
-                    tp[0] = c[0] ? p : tp[0];
-                    tb[0] = c[0] ? j : tb[0];
-                }
-            }
-            // merge the LPW partial lists of a window (lanes mw + WB q): keep the best 8 of each pair
-#pragma unroll
-            for (int r = 1; r < LPW; r <<= 1) {
-                double op[K];
-                int ob[K];
-#pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    op[s] = __shfl_xor(tp[s], WB * r, 64);
-                    ob[s] = __shfl_xor(tb[s], WB * r, 64);
-                }
-                // best of mine[s] and the partner's [K-1-s]: the 8 best of the union, in bitonic order
-#pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    const bool t = kbetter(op[K - 1 - s], ob[K - 1 - s], tp[s], tb[s]);
-                    tp[s] = t ? op[K - 1 - s] : tp[s];
-                    tb[s] = t ? ob[K - 1 - s] : tb[s];
-                }
-                // bitonic half-cleaners: best first
-#pragma unroll
-                for (int h = K / 2; h > 0; h >>= 1)
-#pragma unroll
-                    for (int i = 0; i < K; ++i)
-                        if ((i & h) == 0) {
-                            const bool t = kbetter(tp[i + h], tb[i + h], tp[i], tb[i]);
-                            const double pa = tp[i], pb = tp[i + h];
-                            const int ba = tb[i], bb = tb[i + h];
-                            tp[i] = t ? pb : pa;
-                            tp[i + h] = t ? pa : pb;
-                            tb[i] = t ? bb : ba;
-                            tb[i + h] = t ? ba : bb;
-                        }
-            }
-            // records of window (wi - slot + mw): part mq writes slots mq * K / LPW ..
-            if (wok) {
-                double *o = rec + (int64_t)(wi - slot + mw) * (4 * kk);
-                constexpr int PER = K / LPW > 0 ? K / LPW : 1;
-#pragma unroll
-                for (int e = 0; e < PER; ++e) {
-                    const int s = mq * PER + e;
-                    // slot s of the lists by selects (register arrays are indexed at compile time only)
-                    double ps = tp[0];
-                    int bs = tb[0];
-#pragma unroll
-                    for (int i = 1; i < K; ++i) {
-                        ps = s == i ? tp[i] : ps;
-                        bs = s == i ? tb[i] : bs;
-                    }
-                    if (s < K && s < kk) {
-                        const bool real = bs != kEmpty;
-                        d2 X = d2{0.0, 0.0};
-                        if (real) X = xs[mw * sp + bs];
-                        typedef double d4 __attribute__((ext_vector_type(4)));
-                        *reinterpret_cast<d4 *>(o + 4 * s) =
-                            real ? d4{(double)(kmin + bs), ps, X.x, X.y} : d4{-1.0, -1.0, 0.0, 0.0};
-                    }
-                }
-            }
-            __syncthreads();  // the scan's reads before the next batch's writes
-        }
-    }
-}
-
-template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
-    const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
-    hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0, s,
-                       a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int nb = (a.span + 63) / 64;
-    // transposed scan for k <= 8 and bands of <= 256 bins (staged batch: WB windows x <= 64 NB bins); the
-    // 512-bin form (NB = 8: 80 tracker registers per lane) stays on the one-wave scan
-    if (a.topk <= kTopkT && a.variant == 0 && nb <= 4) {
-        if (nb <= 1) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 1, 16>), dim3((unsigned)grid), dim3(64), 0, s, a);
-        else if (nb <= 2) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 2, 16>), dim3((unsigned)grid), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 4, 8>), dim3((unsigned)grid), dim3(64), 0, s, a);
-        return hipGetLastError();
-    }
-    if (nb <= 1) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 1>), dim3((unsigned)grid), dim3(64), 0, s, a);
-    else if (nb <= 2) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 2>), dim3((unsigned)grid), dim3(64), 0, s, a);
-    else if (nb <= 4) hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 4>), dim3((unsigned)grid), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((slide_topk_kernel<LOG2N, NF, DETREND, 8>), dim3((unsigned)grid), dim3(64), 0, s, a);
-    return hipGetLastError();
-}
-
-template <int LOG2N, int NF> hipError_t topk_by_detrend(const SlideArgs &a, hipStream_t s) {
-    return a.detrend == kDetrendMean ? launch_topk_t<LOG2N, NF, kDetrendMean>(a, s)
-                                     : launch_topk_t<LOG2N, NF, kDetrendNone>(a, s);
-}
-
-template <int LOG2N> hipError_t topk_by_nf(const SlideArgs &a, hipStream_t s) {
-    switch (a.nf) {
-    case 1: return topk_by_detrend<LOG2N, 1>(a, s);
-    case 3: return topk_by_detrend<LOG2N, 3>(a, s);
-    case 5: return topk_by_detrend<LOG2N, 5>(a, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-// One launch over every member of the group: segment length from the residency (occupancy API, once
-// per instantiation) and the members' total window count, so that a multi-symbol batch gets the same
-// segments as one long series would (C5: 7 symbols of ~19k windows each seed 4-8x fewer times than
-// as separate launches).
-template <typename T, int LOG2N, int NF, int DETREND>
-hipError_t launch_t(const SlideArgs &a0, const SlideGroup &g0, hipStream_t s) {
-    constexpr int NT = (1 << LOG2N) / (2 * slide_b<LOG2N>());
-    static std::atomic<int> resident{0};
-    int res = resident.load(std::memory_order_relaxed);
-    if (res == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slide_kernel<T, LOG2N, NF, DETREND>, NT, 0) !=
-                hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return hipErrorInvalidValue;
-        res = per_cu * cus > 0 ? per_cu * cus : 256;
-        resident.store(res, std::memory_order_relaxed);
-    }
-    SlideArgs a = a0;
-    SlideGroup g = g0;
-    int64_t total = 0;
-    for (int m = 0; m < g.n; ++m) total += g.n_windows[m];
-    if (a.seg <= 0) {  // ~2 rounds of resident workgroups, 32..256 windows each (sweep: DESIGN.md 4.5)
-        a.seg = (total + 2 * (int64_t)res - 1) / (2 * (int64_t)res);
-        a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
-    }
-    g.blk0[0] = 0;
-    for (int m = 0; m < g.n; ++m) g.blk0[m + 1] = g.blk0[m] + (g.n_windows[m] + a.seg - 1) / a.seg;
-    const int64_t grid = g.blk0[g.n];
-    if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL((slide_kernel<T, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(NT), 0, s, a, g);
-    return hipGetLastError();
-}
-
-template <typename T, int LOG2N, int NF> hipError_t by_detrend(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
-    return a.detrend == kDetrendMean ? launch_t<T, LOG2N, NF, kDetrendMean>(a, g, s)
-                                     : launch_t<T, LOG2N, NF, kDetrendNone>(a, g, s);
-}
-
-template <typename T, int LOG2N> hipError_t by_nf(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
-    switch (a.nf) {
-    case 1: return by_detrend<T, LOG2N, 1>(a, g, s);
-    case 3: return by_detrend<T, LOG2N, 3>(a, g, s);
-    case 5: return by_detrend<T, LOG2N, 5>(a, g, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-template <typename T> hipError_t by_n(const SlideArgs &a, const SlideGroup &g, hipStream_t s) {
-    switch (a.log2n) {
-    case 9: return by_nf<T, 9>(a, g, s);
-    case 10: return by_nf<T, 10>(a, g, s);
-    case 11: return by_nf<T, 11>(a, g, s);
-    case 12: return by_nf<T, 12>(a, g, s);
-    case 13: return by_nf<T, 13>(a, g, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-}  // namespace
 
 hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {
     if (a.n_windows <= 0) return hipSuccess;
@@ -656,11 +11,11 @@ hipError_t launch_slide_topk(const SlideArgs &a, hipStream_t s) {
         a.topk < 1 || a.topk > 64 || !a.ws)
         return hipErrorInvalidValue;
     switch (a.log2n) {
-    case 9: return topk_by_nf<9>(a, s);
-    case 10: return topk_by_nf<10>(a, s);
-    case 11: return topk_by_nf<11>(a, s);
-    case 12: return topk_by_nf<12>(a, s);
-    case 13: return topk_by_nf<13>(a, s);
+    case 9: return launch_slide_topk_l9(a, s);
+    case 10: return launch_slide_topk_l10(a, s);
+    case 11: return launch_slide_topk_l11(a, s);
+    case 12: return launch_slide_topk_l12(a, s);
+    case 13: return launch_slide_topk_l13(a, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -680,7 +35,9 @@ hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream
         return hipErrorInvalidValue;
     for (int m = 0; m < g.n; ++m)
         if (g.n_windows[m] < 0 || !g.series[m] || !g.out[m]) return hipErrorInvalidValue;
-    return a.f32 ? by_n<float>(a, g, s) : by_n<double>(a, g, s);
+    return a.f32 ? launch_slide_group_f32(a, g, s) : launch_slide_group_f64(a, g, s);
 }
+
+hipError_t launch_slide_group_f64(const SlideArgs &a, const SlideGroup &g, hipStream_t s) { return by_n<double>(a, g, s); }
 
 }  // namespace wsp

@@ -81,6 +81,7 @@ struct LargeLaunch {
     int packed;           // 0 power, 1 packed (Re, Im)
     bool f32;
     double iir_alpha, iir_c;
+    int variant;          // 0 auto (fused where it applies), 1 two-pass, 3 fused at two workgroups per CU
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
@@ -122,7 +123,7 @@ struct SlideArgs {
     // top-k records (launch_slide_topk, fp64): bins [kmin, kmin + span), topk slots, seeds workspace
     int kmin, span, topk;
     void *ws;             // ceil(n_windows / seg) * slide_topk_seed_stride(nf, span) double complex
-    int variant;          // top-k scan: 0 = transposed (lane per window, k <= 8), 1 = one wave per window
+    int variant;          // top-k scan: 0 = auto, 1 = one wave per window, 2 / 3 = transposed, 16 / 8 windows per batch
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
 // Grouped launch: several series of the same window length (the symbols of one length in a

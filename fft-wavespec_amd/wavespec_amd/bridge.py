@@ -67,6 +67,7 @@ SIGNATURES = {
     "wsp_plan_set_algorithm": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_get_algorithm": (C.c_int32, [C.c_int64]),
     "wsp_plan_set_slide_segment": (C.c_int32, [C.c_int64, C.c_int64]),
+    "wsp_plan_set_variant": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -78,6 +79,8 @@ SIGNATURES = {
     "wsp_group_execute": (C.c_int32, [C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_void_p]),
     "wsp_group_algorithmic_bytes": (C.c_int64, [C.c_int64]),
     "wsp_group_launches": (C.c_int32, [C.c_int64]),
+    "wsp_group_set_streams": (C.c_int32, [C.c_int64, C.c_int32]),
+    "wsp_group_set_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_group_destroy": (C.c_int32, [C.c_int64]),
     "wsp_version": (C.c_char_p, []),
 }
@@ -314,6 +317,10 @@ class Plan:
         """Tuning: windows per sliding-DFT workgroup (0 = the library's policy)."""
         _check("wsp_plan_set_slide_segment", lib().wsp_plan_set_slide_segment(self.handle, windows))
 
+    def set_variant(self, variant: int) -> None:
+        """Ablation: the hop = 1 top-k scan form (0 auto, 1 one-wave, 2 / 3 transposed 16 / 8 windows)."""
+        _check("wsp_plan_set_variant", lib().wsp_plan_set_variant(self.handle, variant))
+
     def algorithm(self) -> str:
         """What the next execute runs: "fft" or "slide"."""
         return {1: "fft", 2: "slide"}[lib().wsp_plan_get_algorithm(self.handle)]
@@ -360,6 +367,14 @@ class Group:
     @property
     def launches(self) -> int:
         return int(lib().wsp_group_launches(self.handle))
+
+    def set_streams(self, n: int) -> None:
+        """Tuning: fork each execute over n internal streams (1 = the caller's stream only)."""
+        _check("wsp_group_set_streams", lib().wsp_group_set_streams(self.handle, n))
+
+    def set_segment(self, windows: int) -> None:
+        """Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy)."""
+        _check("wsp_group_set_segment", lib().wsp_group_set_segment(self.handle, windows))
 
     def execute(self, d_series, d_out, stream: int = 0) -> None:
         """d_series / d_out: device pointers (ints), one per member."""

@@ -298,6 +298,11 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
+/* Tuning / ablation: the form of the hop = 1 top-k scan by the sliding DFT.
+ * 0 = the library's choice (default); 1 = one wave-wide reduction round per
+ * slot and window; 2 / 3 = the transposed lane-per-window scan (k <= 8, bands
+ * <= 256 bins) staging 16 / 8 windows per batch.  Same records either way. */
+MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
 
@@ -325,6 +330,15 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
 MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
 /* Kernel launches one execute makes (one per window length and 16 members). */
 MTB_API int32_t wsp_group_launches(int64_t group);
+/* Tuning: n_streams > 1 forks every execute from the caller's stream onto n
+ * internal streams (launches assigned greedily by output bytes) and joins
+ * them back into it (events; no host sync), so one window length's last
+ * workgroups overlap the next length's first.  1 (default) = everything on
+ * the caller's stream.  MTB_BAD_ARGS outside 1..8. */
+MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams);
+/* Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy over
+ * each window length's total window count), at most 2048. */
+MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
 MTB_API int32_t wsp_plan_destroy(int64_t plan);
