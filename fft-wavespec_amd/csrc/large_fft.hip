@@ -31,8 +31,11 @@
 // L/WaveSpecZZ_1.0.2.mq5:3040-3053), Kalman by the common pre-pass; the
 // latter two write detrended windows that the column pass reads with hop = N.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "spectrum_dispatch.h"
 
@@ -321,16 +324,19 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
-template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED>
-__global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256>
+__global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
-    constexpr int RB = RowGeo<LOG2M1>::RB;
-    constexpr int M1 = GR::L, M2 = GC::L, TPC = GC::TP, TPR = GR::TP, NB1 = M1 / kCB, NB2 = (M2 / 2) / RB;
-    static_assert(kCB * TPC == 256 && 2 * RB * TPR == 256, "256 threads in both passes");
+    constexpr int M1 = GR::L, M2 = GC::L, TPC = GC::TP, TPR = GR::TP;
+    // NT threads: CB columns per column block, RB rows (+ RB mirror rows) per row block; both fill the
+    // LDS (CB x SLOT or 2 RB x SLOT complex: 70 KiB at NT = 256; at 512 threads the FFT's ~250 VGPRs
+    // spill 350 B/lane), one workgroup per CU
+    constexpr int CB = NT / TPC, RB = NT / (2 * TPR), NB1 = M1 / CB, NB2 = (M2 / 2) / RB;
+    static_assert(CB * TPC == NT && 2 * RB * TPR == NT && NB1 >= 1 && NB2 >= 1, "thread geometry");
     constexpr int64_t M = (int64_t)M1 * M2;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    constexpr int LDS_C = kCB * GC::SLOT, LDS_R = 2 * RB * GR::SLOT;
+    constexpr int LDS_C = CB * GC::SLOT, LDS_R = 2 * RB * GR::SLOT;
     __shared__ cpx<T> lds[LDS_C > LDS_R ? LDS_C : LDS_R];
     const int tid = threadIdx.x;
     const T *__restrict__ series = static_cast<const T *>(a.series);
@@ -339,13 +345,13 @@ __global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
     const int N = 1 << a.log2n;
     using v2 = typename core::V2<T>::t;
     // column pass geometry (col_kernel): column c of the block, transform thread t
-    const int cc = tid % kCB, ct = tid / kCB;
+    const int cc = tid % CB, ct = tid / CB;
     // row pass geometry (row_kernel): slot rho, transform thread t
     const int rho = tid / TPR, rt = tid % TPR;
     v2 raw[16];
-    auto load_cols = [&](int64_t w, int beta) {  // 16 sample pairs of column beta * kCB + cc
+    auto load_cols = [&](int64_t w, int beta) {  // 16 sample pairs of column beta * CB + cc
         const T *__restrict__ xw = series + w * a.hop;
-        const int n1 = beta * kCB + cc;
+        const int n1 = beta * CB + cc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = n1 + M1 * (ct + TPC * r);
@@ -365,13 +371,12 @@ __global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) nxt[r] = yr[rt + TPR * r];
     };
-    int64_t w = blockIdx.x;
-    if (w < a.nwin) load_cols(w, 0);
-    for (; w < a.nwin; w += gridDim.x) {
-        // ---- column pass: NB1 blocks of kCB columns
+    for (int64_t w = blockIdx.x; w < a.nwin; w += gridDim.x) {
+        // ---- column pass: NB1 blocks of CB columns
+        load_cols(w, 0);
         const double mean = MEAN ? a.means[w] : 0.0;
         for (int beta = 0; beta < NB1; ++beta) {
-            const int n1 = beta * kCB + cc;
+            const int n1 = beta * CB + cc;
             double cw = 1.0, sw = 0.0;
             if constexpr (kCos) sincos(a.inv_theta * (double)(2 * (n1 + M1 * ct)), &sw, &cw);
             int nb = n1 + M1 * ct;
@@ -403,9 +408,8 @@ __global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
                 }
                 v[r] = {(T)xa, (T)xb};
             }
-            // next block's samples (or the next window's first block) in flight during this FFT
+            // next block's samples in flight during this FFT (not across the row pass: registers)
             if (beta + 1 < NB1) load_cols(w, beta + 1);
-            else if (w + gridDim.x < a.nwin) load_cols(w + gridDim.x, 0);
             wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
             constexpr int R = last_radix<LOG2M2>();
             const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(256) void fused_kernel(ColArgs a, RowArgs ra) {
                 }
             __syncthreads();
             T *__restrict__ ow = static_cast<T *>(ra.out) + w * (int64_t)(PACKED ? 2 * M : M);
-            for (int ii = tid; ii < M1 * 2 * RB; ii += 256) {
+            for (int ii = tid; ii < M1 * 2 * RB; ii += NT) {
                 const int sl = ii % (2 * RB), k1 = ii / (2 * RB);
                 const int il = sl < RB ? sl : sl - RB, l2 = beta2 * RB + il;
                 const int64_t k = (sl < RB ? l2 : (l2 == 0 ? M2 / 2 : M2 - l2)) + (int64_t)M2 * k1;
@@ -625,15 +629,15 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
     return L.packed ? row_launch<T, LM1, LM2, true>(ra, s) : row_launch<T, LM1, LM2, false>(ra, s);
 }
 
-// the fused form for M2 = 256 (N = 65536, 131072): one launch over every window
+// the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablation, variant 3)
 template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0,
                                                        const large::RowArgs &ra, int wclass, bool mean, hipStream_t s) {
     large::ColArgs ca = ca0;
     ca.w0 = 0;
     ca.nwin = L.n_windows;
-    // workgroups in flight: one per CU by default (slots stay in the Infinity Cache), two with variant 3;
-    // never more slots than the plan workspace holds (a chunk of windows)
-    const int per_cu = L.variant == 3 ? 2 : 1;
+    // workgroups in flight: one per CU (the slots stay in the Infinity Cache; two per CU measured 1.90 ms
+    // against 1.51), never more slots than the plan workspace holds (a chunk of windows)
+    const int per_cu = 1;
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>({L.n_windows, L.chunk, (int64_t)per_cu * cu_count()}));
     hipError_t e = hipSuccess;
     using namespace core;
@@ -654,6 +658,57 @@ template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, con
 #undef FUSED
     e = hipGetLastError();
     return e;
+}
+
+hipError_t chunk_dispatch(int log2m, const LargeLaunch &L, const large::ColArgs &ca, const large::RowArgs &ra,
+                          int wclass, bool mean, hipStream_t s, bool f32);
+
+// two internal streams per device for the pipelined ablation (created once, never destroyed)
+hipStream_t aux_stream(int i) {
+    static std::mutex mu;
+    static std::map<int, std::array<hipStream_t, 2>> streams;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = streams.find(dev);
+    if (it == streams.end()) {
+        std::array<hipStream_t, 2> a{};
+        for (auto &x : a)
+            if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        it = streams.emplace(dev, a).first;
+    }
+    return it->second[i];
+}
+
+template <typename T>
+hipError_t pipelined_t(const LargeLaunch &L, large::ColArgs ca, large::RowArgs ra, int wclass, bool mean, int log2m,
+                       hipStream_t s) {
+    const int64_t chunk = std::max<int64_t>(1, L.chunk / 4);
+    hipStream_t st[2] = {aux_stream(0), aux_stream(1)};
+    if (!st[0] || !st[1]) return hipErrorInvalidValue;
+    hipEvent_t fork, join[2];
+    hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    for (auto &j : join)
+        if ((e = hipEventCreateWithFlags(&j, hipEventDisableTiming)) != hipSuccess) return e;
+    (void)hipEventRecord(fork, s);
+    for (auto x : st) (void)hipStreamWaitEvent(x, fork, 0);
+    const size_t ybytes = (size_t)chunk * ((size_t)1 << log2m) * sizeof(core::cpx<T>);
+    int64_t i = 0;
+    for (int64_t w0 = 0; w0 < L.n_windows; w0 += chunk, ++i) {
+        ca.w0 = ra.w0 = w0;
+        ca.nwin = ra.nwin = std::min<int64_t>(chunk, L.n_windows - w0);
+        ca.y = static_cast<char *>(L.y) + (i % 2) * ybytes;  // two Y buffers (the workspace holds 4 chunks)
+        ra.y = ca.y;
+        if ((e = chunk_dispatch(log2m, L, ca, ra, wclass, mean, st[i % 2], sizeof(T) == 4)) != hipSuccess) return e;
+    }
+    for (int k = 0; k < 2; ++k) {
+        (void)hipEventRecord(join[k], st[k]);
+        (void)hipStreamWaitEvent(s, join[k], 0);
+    }
+    (void)hipEventDestroy(fork);
+    for (auto j : join) (void)hipEventDestroy(j);
+    return hipGetLastError();
 }
 
 template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
@@ -710,11 +765,15 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     ra.packed = L.packed;
     ra.w0 = 0;
     ra.nwin = L.n_windows;
-    // fused form (one launch, Y through the Infinity Cache) for N = 65536 / 131072; variant 1 forces the
-    // two-pass form (ablation)
-    if (L.variant != 1 && (log2m == 15 || log2m == 16))
+    // ablations: variant 3 = the fused one-workgroup-per-window form (N = 65536 / 131072; 1.51 ms against
+    // 1.44 for the two-pass form at 4096 x 65536: one wave per SIMD at ~250 VGPRs cannot hide the FFT's
+    // latencies); variant 2 = two-pass over chunks of a quarter of the default size, alternating between
+    // two internal streams so that the column pass of chunk i + 1 runs beside the row pass of chunk i
+    // while chunk i's column results are still in the Infinity Cache
+    if (L.variant == 3 && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8>(L, ca, ra, wclass, means != nullptr, s);
+    if (L.variant == 2) return pipelined_t<T>(L, ca, ra, wclass, means != nullptr, log2m, s);
     for (int64_t w0 = 0; w0 < L.n_windows; w0 += L.chunk) {
         ca.w0 = ra.w0 = w0;
         ca.nwin = ra.nwin = std::min<int64_t>(L.chunk, L.n_windows - w0);
@@ -728,6 +787,26 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t chunk_dispatch(int log2m, const LargeLaunch &L, const large::ColArgs &ca, const large::RowArgs &ra,
+                          int wclass, bool mean, hipStream_t s, bool f32) {
+    if (f32) {
+        switch (log2m) {
+        case 14: return chunk_launch<float, 7, 7>(L, ca, ra, wclass, mean, s);
+        case 15: return chunk_launch<float, 7, 8>(L, ca, ra, wclass, mean, s);
+        case 16: return chunk_launch<float, 8, 8>(L, ca, ra, wclass, mean, s);
+        case 17: return chunk_launch<float, 8, 9>(L, ca, ra, wclass, mean, s);
+        default: return hipErrorInvalidValue;
+        }
+    }
+    switch (log2m) {
+    case 14: return chunk_launch<double, 7, 7>(L, ca, ra, wclass, mean, s);
+    case 15: return chunk_launch<double, 7, 8>(L, ca, ra, wclass, mean, s);
+    case 16: return chunk_launch<double, 8, 8>(L, ca, ra, wclass, mean, s);
+    case 17: return chunk_launch<double, 8, 9>(L, ca, ra, wclass, mean, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace

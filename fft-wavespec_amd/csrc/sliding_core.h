@@ -412,6 +412,22 @@ constexpr int kTopkT = 8;  // slots of the transposed scan (the reference's top 
 
 __device__ __forceinline__ bool kbetter(double pa, int ba, double pb, int bb) { return pa > pb || (pa == pb && ba < bb); }
 
+// the reference's insertion (gpuopt-nodetrend.mq5:545-552): the first slot s with p > tp[s] takes (p, j),
+// the slots after it shift down one; branch-free over the sorted register list
+template <int K> __device__ __forceinline__ void topk_insert(double (&tp)[K], int (&tb)[K], double p, int j) {
+    bool c[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) c[s] = p > tp[s];
+#pragma unroll
+    for (int s = K - 1; s > 0; --s) {
+        tp[s] = c[s] ? (c[s - 1] ? tp[s - 1] : p) : tp[s];
+        tb[s] = c[s] ? (c[s - 1] ? tb[s - 1] : j) : tb[s];
+    }
+    tp[0] = c[0] ? p : tp[0];
+    tb[0] = c[0] ? j : tb[0];
+}
+constexpr int kCand = 8;  // candidate list entries per lane of the transposed scan (+1 scratch slot)
+
 template <int LOG2N, int NF, int DETREND, int NB, int WB>
 __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
     constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128, LPW = 64 / WB, K = kTopkT;
@@ -442,11 +458,15 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
     const d2 sl = ws[NF * span];
     double sum = sl.x;
     const double lvl = sl.y;
-    // the scan's lane roles: window mw of the staged batch, band part mq: bins [q0, q1)
+    // the scan's lane roles: window mw of the staged batch, band part mq: bins mq, mq + LPW, ...
     const int mw = l % WB, mq = l / WB;
-    const int qs = (span + LPW - 1) / LPW, q0 = mq * qs, q1 = q0 + qs < span ? q0 + qs : span;
     double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
     const int kk = a.topk;
+    double tp[K];
+    int tb[K], pb[K];
+    bool have_prev = false;
+    double *cp = reinterpret_cast<double *>(xs + WB * sp);  // candidate lists [kCand + 1][64] powers, bins
+    int *cj = reinterpret_cast<int *>(cp + (kCand + 1) * 64);
     for (int c0 = 0; c0 < len; c0 += CHT) {
         const int clen = len - c0 < CHT ? len - c0 : CHT;
         if (c0) __syncthreads();
@@ -463,43 +483,72 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
                 for (int f = 1; f < NF; ++f) X += tr[b][f];
                 if constexpr (DETREND == kDetrendMean) X -= mwv * hk[b];
                 const int j = l + 64 * b;
+#ifdef WSP_TOPK_ABLATION
+                if (a.variant == 5) continue;  // timing ablation: slide only
+#endif
                 if (j < span) xs[slot * sp + j] = X;
             }
             if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
             if (slot != WB - 1 && wi + 1 < len) continue;
+#ifdef WSP_TOPK_ABLATION
+            if (a.variant >= 4) continue;  // timing ablation: no scan, no records
+#endif
             // ---- scan the staged batch: windows wi - slot .. wi
             __syncthreads();
-            double tp[K];
-            int tb[K];
-#pragma unroll
-            for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
             const bool wok = mw <= slot;
+            const d2 *row = xs + mw * sp;
+            // Threshold: the powers, in THIS window, of the 8 bins that won this lane's window slot in the
+            // previous batch (window - WB).  They are 8 distinct bins of this window, so their minimum is
+            // at most its 8th largest power: every bin of its top 8 -- ties at the 8th included -- has
+            // p >= tau.  Only those candidates take the 8-slot insertion; the rest cost a compare.
+            double tau = -1.0;
+            if (have_prev && wok) {
+                tau = __builtin_inf();
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    const d2 X = row[pb[s] != kEmpty ? pb[s] : 0];
+                    tau = fmin(tau, pb[s] != kEmpty ? X.x * X.x + X.y * X.y : -1.0);
+                }
+            }
+            // candidates of this lane's part (bins mq, mq + LPW, ...: ascending, interleaved so that the
+            // strong low bins spread over the parts) into the lane's LDS list [C + 1][64]
+            int cnt = 0;
             if (wok) {
-                const d2 *row = xs + mw * sp;
-                // four bins per round, their LDS reads issued together (one exposed LDS latency per four
-                // bins instead of per bin); bins past q1 enter as power -1 and never take a slot
-                for (int j = q0; j < q1; j += 4) {
+                for (int j = mq; j < span; j += 4 * LPW) {
                     double pw[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const d2 X = row[j + i < q1 ? j + i : q1 - 1];
-                        pw[i] = j + i < q1 ? X.x * X.x + X.y * X.y : -1.0;
+                        const int jj = j + i * LPW;
+                        const d2 X = row[jj < span ? jj : mq];
+                        pw[i] = jj < span ? X.x * X.x + X.y * X.y : -1.0;
                     }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        // insertion as the reference: first slot s with p > tp[s] takes it, the rest shift down
-                        const double p = pw[i];
-                        bool c[K];
-#pragma unroll
-                        for (int s = 0; s < K; ++s) c[s] = p > tp[s];
-#pragma unroll
-                        for (int s = K - 1; s > 0; --s) {
-                            tp[s] = c[s] ? (c[s - 1] ? tp[s - 1] : p) : tp[s];
-                            tb[s] = c[s] ? (c[s - 1] ? tb[s - 1] : j + i) : tb[s];
-                        }
-                        tp[0] = c[0] ? p : tp[0];
-                        tb[0] = c[0] ? j + i : tb[0];
+                        const int at = cnt < kCand ? cnt : kCand;  // slot kCand: scratch for overflow
+                        cp[at * 64 + l] = pw[i];
+                        cj[at * 64 + l] = j + i * LPW;
+                        cnt += pw[i] >= tau ? 1 : 0;
                     }
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
+            if (__ballot(cnt > kCand) == 0) {
+                for (int i = 0; __ballot(i < cnt) != 0; ++i) {  // the candidates, in ascending bin order
+                    const bool on = i < cnt;
+                    topk_insert<K>(tp, tb, on ? cp[i * 64 + l] : -1.0, on ? cj[i * 64 + l] : kEmpty);
+                }
+            } else if (wok) {  // a part with more candidates than the list holds (first batch of a segment): all bins
+                for (int j = mq; j < span; j += 4 * LPW) {
+                    double pw[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int jj = j + i * LPW;
+                        const d2 X = row[jj < span ? jj : mq];
+                        pw[i] = jj < span ? X.x * X.x + X.y * X.y : -1.0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) topk_insert<K>(tp, tb, pw[i], j + i * LPW);
                 }
             }
             // merge the LPW partial lists of a window (lanes mw + WB q): keep the best 8 of each pair
@@ -534,6 +583,9 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
                             tb[i + h] = t ? ba : bb;
                         }
             }
+#pragma unroll
+            for (int s = 0; s < K; ++s) pb[s] = tb[s];  // this slot's winners: the next batch's threshold bins
+            have_prev = true;
             // records of window (wi - slot + mw): part mq writes slots mq * K / LPW ..
             if (wok) {
                 double *o = rec + (int64_t)(wi - slot + mw) * (4 * kk);
@@ -564,6 +616,159 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
     }
 }
 
+// ---- the same records by a probe threshold (default for k <= 8 and bands <= 256 bins).
+// The wave slides its band's trackers bin-major (lane l: bins kmin + l + 64 b) and, per window, keeps
+// only the bins that can be in the top k: tau = the smallest power, in THIS window, of the k bins that won
+// the same slot of the previous batch (WB windows earlier; the segment's first window seeds every slot).
+// Those are k distinct bins of this window, so tau is at most its k-th largest power and every member of
+// its top k -- ties at the k-th included -- has p >= tau (compared on the high words: a superset).  The
+// probes live in registers, one bit per slot in the owner lane's mask, so tau is one 32-bit wave min.
+// The candidates (8.4 per window on average at C4, 11 at the 99th percentile) go to the slot's list in LDS
+// in ascending bin order (ballot + mbcnt); after WB windows each lane takes one window and runs the
+// reference's k-slot insertion (strict '>', gpuopt-nodetrend.mq5:545-552) over its list only.  A window
+// with more than kPCand candidates, or the segment's first, is scanned exactly by the one-wave reduction
+// (core::topk_wave64), whose winners then probe that slot.
+constexpr int kPCand = 16;  // candidate list entries per window
+
+template <int LOG2N, int NF, int DETREND, int NB, int WB>
+__global__ __launch_bounds__(64) void slide_topk_p_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128, K = kTopkT, C = kPCand;
+    constexpr int kEmpty = 0x7fffffff;
+    static_assert(WB <= 32 && CHT % WB == 0, "one lane and one mask bit per window of a batch");
+    __shared__ double u[CHT * REC];
+    __shared__ core::cpx<double> xb[64 * NB];  // the fallback's band
+    __shared__ int win[K];                     // the fallback's winners (band index, -1 empty)
+    __shared__ unsigned nm[64 * NB];           // next batch's probe bits per band bin
+    __shared__ int cnt[WB];                    // candidates per slot, -1: the fallback wrote the record
+    __shared__ d2 cx[WB * C];                  // candidates' X, per slot in ascending bin order
+    __shared__ int cb[WB * C];                 // candidates' band indices
+    const int l = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
+    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
+    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
+    const d2 *__restrict__ hwin = omega + NF * M;
+    const d2 *__restrict__ ws = static_cast<const d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int span = a.span, kmin = a.kmin;
+    d2 tr[NB][NF], om[NB][NF], hk[NB];
+    unsigned mask[NB];  // bit s: this lane's bin of slot b is one of slot s's probes
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = l + 64 * b;
+        const bool ok = j < span;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            tr[b][f] = ok ? ws[f * span + j] : d2{0.0, 0.0};
+            om[b][f] = ok ? omega[f * M + kmin + j] : d2{1.0, 0.0};
+        }
+        hk[b] = (DETREND == kDetrendMean && ok) ? hwin[kmin + j] : d2{0.0, 0.0};
+        mask[b] = 0u;
+        nm[j] = 0u;
+    }
+    const d2 sl = ws[NF * span];
+    double sum = sl.x;
+    const double lvl = sl.y;
+    double *__restrict__ rec = static_cast<double *>(a.out) + w0 * (int64_t)(4 * a.topk);
+    const int kk = a.topk;
+    const bool probes = span >= kk;  // every window's winners are min(k, span) real bins
+    for (int c0 = 0; c0 < len; c0 += CHT) {
+        const int clen = len - c0 < CHT ? len - c0 : CHT;
+        __syncthreads();
+        stage_uniforms<double, NF, N>(a, x, lvl, c0, clen, len, u, l, 64);
+        __syncthreads();
+#pragma unroll 1
+        for (int st = 0; st < clen; ++st) {
+            const int wi = c0 + st, slot = wi % WB;
+            const double mwv = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
+            d2 X[NB];
+            int ph[NB];  // high words of the powers (non-negative doubles order as their bits); INT_MIN outside
+            int mh = 0x7fffffff;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                d2 v = tr[b][0];
+#pragma unroll
+                for (int f = 1; f < NF; ++f) v += tr[b][f];
+                if constexpr (DETREND == kDetrendMean) v -= mwv * hk[b];
+                X[b] = v;
+                const double p = v.x * v.x + v.y * v.y;
+                ph[b] = l + 64 * b < span ? (int)(__builtin_bit_cast(unsigned long long, p) >> 32) : INT_MIN;
+                if ((mask[b] >> slot) & 1u) mh = min(mh, ph[b]);
+            }
+            const int th = (wi > 0 && probes) ? core::wave_min64(mh) : 0;
+            unsigned long long bal[NB];
+            int total = 0;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                bal[b] = __ballot(ph[b] >= th - 1);  // one high-word step of slack: any contraction of |X|^2
+                total += __popcll(bal[b]);
+            }
+            if (wi > 0 && total <= C) {
+                int base = 0;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    if ((bal[b] >> l) & 1) {
+                        const int pos = slot * C + base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal[b] >> 32),
+                                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)bal[b], 0u));
+                        cx[pos] = X[b];
+                        cb[pos] = l + 64 * b;
+                    }
+                    base += __popcll(bal[b]);
+                }
+                if (l == 0) cnt[slot] = total;
+            } else {  // exact one-wave scan of this window; its winners probe the slot from now on
+#pragma unroll
+                for (int b = 0; b < NB; ++b) xb[l + 64 * b] = core::cpx<double>{X[b].x, X[b].y};
+                __syncthreads();
+                core::topk_wave64<NB, double>(xb, kmin, span, kk, l, rec + (int64_t)wi * (4 * kk), true, win);
+                if (l == 0) cnt[slot] = -1;
+                __syncthreads();
+                if (l < kk && win[l] >= 0) atomicOr(&nm[win[l]], 1u << slot);
+                __syncthreads();
+                if (wi == 0) {  // the segment's first window probes every slot of the first batch
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) mask[b] = nm[l + 64 * b] ? 0xffffffffu : 0u;
+                }
+            }
+            if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
+            if (slot != WB - 1 && wi + 1 < len) continue;
+            // ---- the staged batch, one lane per window: windows wi - slot .. wi
+            __syncthreads();
+            const int n = l <= slot ? cnt[l] : -1;
+            double tp[K];
+            int tb[K];
+#pragma unroll
+            for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
+            for (int i = 0; __ballot(i < n) != 0; ++i) {
+                const bool on = i < n;
+                const d2 v = cx[l * C + (on ? i : 0)];
+                topk_insert<K>(tp, tb, on ? v.x * v.x + v.y * v.y : -1.0, on ? i : kEmpty);  // i: ascending bins
+            }
+            if (n >= 0) {
+                double *o = rec + (int64_t)(wi - slot + l) * (4 * kk);
+                typedef double d4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    if (s < kk) {
+                        const bool real = tb[s] != kEmpty;
+                        const int ci = real ? l * C + tb[s] : 0;
+                        const d2 v = cx[ci];
+                        const int bj = cb[ci];
+                        *reinterpret_cast<d4 *>(o + 4 * s) = real ? d4{(double)(kmin + bj), tp[s], v.x, v.y} : d4{-1.0, -1.0, 0.0, 0.0};
+                        if (real) atomicOr(&nm[bj], 1u << l);
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {  // the batch's winners become the next batch's probes
+                mask[b] = nm[l + 64 * b];
+                nm[l + 64 * b] = 0u;
+            }
+        }
+    }
+}
+
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
     hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0, s,
@@ -576,9 +781,16 @@ template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideAr
     // staged batch (4 lanes per window, 2 merge rounds) while the batch takes <= 16 KiB of LDS, else 8
     // (variant 2 / 3 force 16 / 8: ablations)
     const size_t row = (size_t)(a.span | 1) * 2 * sizeof(double);
-    const int wb = a.variant == 2 ? 16 : (a.variant == 3 ? 8 : (16 * row <= (16u << 10) ? 16 : 8));
+    const int wb = (a.variant == 2 || a.variant >= 4) ? 16 : (a.variant == 3 ? 8 : (16 * row <= (16u << 10) ? 16 : 8));
+    static_assert(kCand >= 1, "candidate list");
+    if (a.topk <= kTopkT && a.variant == 0 && nb <= 4) {  // probe threshold, 32 windows per batch
+        if (nb <= 1) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 1, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        else if (nb <= 2) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 2, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 4, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.topk <= kTopkT && a.variant != 1 && nb <= 4) {
-        const size_t lds = (size_t)wb * row;
+        const size_t lds = (size_t)wb * row + (size_t)(kCand + 1) * 64 * (sizeof(double) + sizeof(int));
         if (wb == 16) {
             if (nb <= 1) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 1, 16>), dim3((unsigned)grid), dim3(64), lds, s, a);
             else if (nb <= 2) hipLaunchKernelGGL((slide_topk_t_kernel<LOG2N, NF, DETREND, 2, 16>), dim3((unsigned)grid), dim3(64), lds, s, a);

@@ -496,7 +496,8 @@ __device__ __forceinline__ int wave_min64(int b) {
 // takes the min-over-bins reduction.  Lane r keeps round r's winner; lanes < k write the records
 // at the end (one contiguous 4k-element row).
 template <int NB, typename T>
-__device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span, int k, int lane, T *rec, bool active) {
+__device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span, int k, int lane, T *rec, bool active,
+                                            int *winners = nullptr) {
     // the lane's NB candidates sorted once (power desc, bin asc): its best is always p[0] and
     // retiring it is a shift, not a rescan
     T p[NB];
@@ -581,6 +582,7 @@ __device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span
             p[NB - 1] = T(-1);
         }
     }
+    if (winners && lane < k) winners[lane] = my_j;  // band index of slot `lane`, -1 when empty
     if (active && lane < k) {
         T *o = rec + 4 * lane;
         if (my_j >= 0) {

@@ -81,7 +81,7 @@ struct LargeLaunch {
     int packed;           // 0 power, 1 packed (Re, Im)
     bool f32;
     double iir_alpha, iir_c;
-    int variant;          // 0 auto (fused where it applies), 1 two-pass, 3 fused at two workgroups per CU
+    int variant;          // ablations: 0 default (two-pass), 2 pipelined quarter chunks on two streams, 3 fused
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,

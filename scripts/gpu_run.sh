@@ -92,8 +92,9 @@ print('$cfg', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g wi
         cat $O/kalman_bench.log
         ;;
     harness)
-        run 300 $O/harness_${val%%,*}.log $O/harness_${val%%,*}.log python3 scripts/${val//,/ }
-        cat $O/harness_${val%%,*}.log
+        hl=$O/harness_${val//,/_}.log
+        run 300 $hl $hl python3 scripts/${val//,/ }
+        cat $hl
         ;;
     *)
         echo "unknown step $step"

@@ -127,3 +127,34 @@ def test_large_device_plan(gpu_session):
         plan.close()
     assert oracle.rel_err(p[:8], ref(s[:8 * n], n, n, "kalman", "hann")) <= TOL["f64"]
     assert oracle.rel_err(p[-4:], ref(s[-4 * n:], n, n, "kalman", "hann")) <= TOL["f64"]
+
+
+@pytest.mark.parametrize("n,variant,detrend,window,output", [
+    (65536, 2, "none", "hann", "power"), (65536, 3, "none", "hann", "power"), (65536, 3, "mean", "blackman", "packed"),
+    (131072, 3, "none", "bartlett", "power"), (131072, 2, "iir", "hann", "power"), (32768, 2, "mean", "hamming", "power")])
+def test_large_variants_identical(gpu_session, n, variant, detrend, window, output):
+    """The large-N ablation forms (wsp_plan_set_variant: 2 = two-pass over quarter chunks pipelined on two
+    internal streams, 3 = the fused one-workgroup-per-window kernel) run the same arithmetic as the default
+    two-pass form: identical records (variant 2) or within 1e-13 (variant 3), and the oracle's bar."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    nwin = 37
+    s = synth.random_walk(nwin * n, seed=n // 1024 + variant)
+    d_s = torch.from_numpy(s).to(dev)
+    period = 1024 if detrend == "iir" else 0
+    outs = []
+    for v in (0, variant):
+        plan = bridge.Plan(0, n, n, nwin, detrend, window, period, "f64", output)
+        plan.set_variant(v)
+        o = torch.empty(nwin * plan.record, dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(o.cpu().numpy().reshape(nwin, plan.record))
+        plan.close()
+    if variant == 2:  # the same kernels over other chunk boundaries: identical
+        assert np.array_equal(outs[0], outs[1])
+    else:  # the fused kernel: the same operations, contracted differently by the compiler
+        den = np.abs(outs[0]).max(axis=1, keepdims=True)
+        assert np.max(np.abs(outs[1] - outs[0]) / den) <= 1e-13
+    if output == "power":
+        assert oracle.rel_err(outs[1][:4], ref(s[:4 * n], n, n, detrend, window, period)) <= TOL["f64"]
