@@ -324,7 +324,7 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
-template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256>
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true>
 __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
@@ -373,9 +373,10 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     };
     for (int64_t w = blockIdx.x; w < a.nwin; w += gridDim.x) {
         // ---- column pass: NB1 blocks of CB columns
-        load_cols(w, 0);
+        if (PF) load_cols(w, 0);
         const double mean = MEAN ? a.means[w] : 0.0;
         for (int beta = 0; beta < NB1; ++beta) {
+            if (!PF) load_cols(w, beta);
             const int n1 = beta * CB + cc;
             double cw = 1.0, sw = 0.0;
             if constexpr (kCos) sincos(a.inv_theta * (double)(2 * (n1 + M1 * ct)), &sw, &cw);
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 v[r] = {(T)xa, (T)xb};
             }
             // next block's samples in flight during this FFT (not across the row pass: registers)
-            if (beta + 1 < NB1) load_cols(w, beta + 1);
+            if (PF && beta + 1 < NB1) load_cols(w, beta + 1);
             wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
             constexpr int R = last_radix<LOG2M2>();
             const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
@@ -426,15 +427,16 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
         }
         __syncthreads();  // Y of this window complete and visible to the workgroup
         // ---- row pass: NB2 blocks of RB rows + their mirror rows
-        load_rows(0);
+        if (PF) load_rows(0);
         for (int beta2 = 0; beta2 < NB2; ++beta2) {
+            if (!PF) load_rows(beta2);
             const int i = rho < RB ? rho : rho - RB, lo = beta2 * RB + i;
             const int row = rho < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
             cpx<T> *slot = lds + rho * GR::SLOT;
             cpx<T> v[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = nxt[r];
-            if (beta2 + 1 < NB2) load_rows(beta2 + 1);
+            if (PF && beta2 + 1 < NB2) load_rows(beta2 + 1);
             wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
             constexpr int R = last_radix<LOG2M1>();
 #pragma unroll
@@ -629,9 +631,11 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
     return L.packed ? row_launch<T, LM1, LM2, true>(ra, s) : row_launch<T, LM1, LM2, false>(ra, s);
 }
 
-// the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablation, variant 3)
-template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0,
-                                                       const large::RowArgs &ra, int wclass, bool mean, hipStream_t s) {
+// the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablations: variant 3 =
+// 512 threads without register prefetch, two waves per SIMD; variant 4 = 256 threads with prefetch)
+template <typename T, int LM1, int NT, bool PF>
+hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const large::RowArgs &ra, int wclass, bool mean,
+                        hipStream_t s) {
     large::ColArgs ca = ca0;
     ca.w0 = 0;
     ca.nwin = L.n_windows;
@@ -639,15 +643,14 @@ template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, con
     // against 1.51), never more slots than the plan workspace holds (a chunk of windows)
     const int per_cu = 1;
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>({L.n_windows, L.chunk, (int64_t)per_cu * cu_count()}));
-    hipError_t e = hipSuccess;
     using namespace core;
 #define FUSED(WC)                                                                                                          \
     if (mean) {                                                                                                            \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     } else {                                                                                                               \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false>), dim3((unsigned)grid), dim3(256), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     }
     switch (wclass) {
     case kWinCos: FUSED(kWinCos); break;
@@ -656,8 +659,7 @@ template <typename T, int LM1> hipError_t fused_launch(const LargeLaunch &L, con
     default: FUSED(kWinNone); break;
     }
 #undef FUSED
-    e = hipGetLastError();
-    return e;
+    return hipGetLastError();
 }
 
 hipError_t chunk_dispatch(int log2m, const LargeLaunch &L, const large::ColArgs &ca, const large::RowArgs &ra,
@@ -771,8 +773,11 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     // two internal streams so that the column pass of chunk i + 1 runs beside the row pass of chunk i
     // while chunk i's column results are still in the Infinity Cache
     if (L.variant == 3 && (log2m == 15 || log2m == 16))
-        return log2m == 15 ? fused_launch<T, 7>(L, ca, ra, wclass, means != nullptr, s)
-                           : fused_launch<T, 8>(L, ca, ra, wclass, means != nullptr, s);
+        return log2m == 15 ? fused_launch<T, 7, 512, false>(L, ca, ra, wclass, means != nullptr, s)
+                           : fused_launch<T, 8, 512, false>(L, ca, ra, wclass, means != nullptr, s);
+    if (L.variant == 4 && (log2m == 15 || log2m == 16))
+        return log2m == 15 ? fused_launch<T, 7, 256, true>(L, ca, ra, wclass, means != nullptr, s)
+                           : fused_launch<T, 8, 256, true>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 2) return pipelined_t<T>(L, ca, ra, wclass, means != nullptr, log2m, s);
     for (int64_t w0 = 0; w0 < L.n_windows; w0 += L.chunk) {
         ca.w0 = ra.w0 = w0;

@@ -81,7 +81,7 @@ struct LargeLaunch {
     int packed;           // 0 power, 1 packed (Re, Im)
     bool f32;
     double iir_alpha, iir_c;
-    int variant;          // ablations: 0 default (two-pass), 2 pipelined quarter chunks on two streams, 3 fused
+    int variant;          // ablations: 0 default (two-pass), 2 pipelined quarter chunks on two streams, 3 fused (512 threads, no prefetch), 4 fused (256 threads, prefetch)
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
