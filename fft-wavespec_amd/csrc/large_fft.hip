@@ -38,6 +38,7 @@
 #include <mutex>
 
 #include "spectrum_dispatch.h"
+#include "wg_fft.h"
 
 namespace wsp {
 namespace large {
@@ -50,62 +51,9 @@ using core::csub;
 using core::dft;
 using core::pad16;
 
-template <int LOG2L> struct LGeo {
-    static constexpr int L = 1 << LOG2L;
-    static constexpr int TP = L / 16;                         // threads per transform
-    static constexpr int NP = LOG2L / 4 + (LOG2L % 4 ? 1 : 0);  // passes
-    static constexpr int radix(int p) { return p < LOG2L / 4 ? 16 : (1 << (LOG2L % 4)); }
-    static constexpr int ns(int p) {
-        int s = 1;
-        for (int i = 0; i < p; ++i) s *= radix(i);
-        return s;
-    }
-    static constexpr int SLOT = L + L / 16;  // padded LDS elements per transform
-    static_assert(LOG2L >= 6 && LOG2L <= 9, "transform length 64 .. 512");
-};
-
-// L-point forward FFT of one transform held by TP threads (16 points each:
-// v[r] = x[t + TP r] on entry).  On exit v[q R + r] = X[b + (L/R) r] with
-// b = t + TP q and R the last pass's radix.  `slot` is this transform's LDS
-// region (SLOT elements); tw = W_N^j, j < N, of a table of period N (twN).
-template <typename T, int LOG2L, int PASS = 1>
-__device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, const cpx<T> *__restrict__ tw, int log2tw) {
-    using G = LGeo<LOG2L>;
-    constexpr int L = G::L, TP = G::TP;
-    if constexpr (PASS == 1) dft<T, 16>(v);  // pass 0: radix 16 over r, no twiddles (Ns = 1)
-    if constexpr (PASS < G::NP) {
-        // write the previous pass's outputs: butterfly b (Ns = ns(PASS-1), R = radix(PASS-1))
-        constexpr int Rp = G::radix(PASS - 1), Nsp = G::ns(PASS - 1);
-#pragma unroll
-        for (int q = 0; q < 16 / Rp; ++q) {
-            const int b = t + TP * q, j = b % Nsp, base = (b / Nsp) * Nsp * Rp + j;
-#pragma unroll
-            for (int r = 0; r < Rp; ++r) slot[pad16(base + Nsp * r)] = v[q * Rp + r];
-        }
-        __syncthreads();
-        constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
-#pragma unroll
-        for (int q = 0; q < 16 / R; ++q) {
-            const int b = t + TP * q, j = b % Ns;
-#pragma unroll
-            for (int r = 0; r < R; ++r) v[q * R + r] = slot[pad16(b + (L / R) * r)];
-            // twiddle W_{Ns R}^{j r} = W_N^{j r N/(Ns R)}: one table entry, powers by products
-            // (<= 15 steps: ~15 ulp)
-            const cpx<T> w1 = tw[(j << log2tw) / (Ns * R)];
-            cpx<T> wr = w1;
-#pragma unroll
-            for (int r = 1; r < R; ++r) {
-                v[q * R + r] = cmul(v[q * R + r], wr);
-                if (r + 1 < R) wr = cmul(wr, w1);
-            }
-            dft<T, R>(v + q * R);
-        }
-        __syncthreads();  // slot reuse by the caller / next pass
-        wg_fft<T, LOG2L, PASS + 1>(v, slot, t, tw, log2tw);
-    }
-}
-
-template <int LOG2L> __device__ __forceinline__ constexpr int last_radix() { return LGeo<LOG2L>::radix(LGeo<LOG2L>::NP - 1); }
+using wg::LGeo;
+using wg::last_radix;
+using wg::wg_fft;
 
 struct ColArgs {
     const void *series;  // window w at series + w*hop
@@ -371,15 +319,27 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) nxt[r] = yr[rt + TPR * r];
     };
+    // window angle of this thread's first sample pair in column block 0 (th * 2 (cc + M1 ct)), and the
+    // rotation by th * 2 CB from one column block to the next (<= NB1 - 1 steps): no sincos in the loop
+    double cw00 = 1.0, sw00 = 0.0, cbd = 1.0, sbd = 0.0;
+    if constexpr (kCos) {
+        sincos(a.inv_theta * (double)(2 * (cc + M1 * ct)), &sw00, &cw00);
+        sincos(a.inv_theta * (double)(2 * CB), &sbd, &cbd);
+    }
     for (int64_t w = blockIdx.x; w < a.nwin; w += gridDim.x) {
         // ---- column pass: NB1 blocks of CB columns
         if (PF) load_cols(w, 0);
         const double mean = MEAN ? a.means[w] : 0.0;
+        double cwb = cw00, swb = sw00;  // angle of column block beta
         for (int beta = 0; beta < NB1; ++beta) {
             if (!PF) load_cols(w, beta);
             const int n1 = beta * CB + cc;
-            double cw = 1.0, sw = 0.0;
-            if constexpr (kCos) sincos(a.inv_theta * (double)(2 * (n1 + M1 * ct)), &sw, &cw);
+            double cw = cwb, sw = swb;
+            if constexpr (kCos) {
+                const double cn = cwb * cbd - swb * sbd;
+                swb = swb * cbd + cwb * sbd;
+                cwb = cn;
+            }
             int nb = n1 + M1 * ct;
             if constexpr (WCLASS == core::kWinBartlett) asm volatile("" : "+v"(nb));
             cpx<T> v[16];
@@ -767,12 +727,14 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     ra.packed = L.packed;
     ra.w0 = 0;
     ra.nwin = L.n_windows;
-    // ablations: variant 3 = the fused one-workgroup-per-window form (N = 65536 / 131072; 1.51 ms against
-    // 1.44 for the two-pass form at 4096 x 65536: one wave per SIMD at ~250 VGPRs cannot hide the FFT's
-    // latencies); variant 2 = two-pass over chunks of a quarter of the default size, alternating between
-    // two internal streams so that the column pass of chunk i + 1 runs beside the row pass of chunk i
-    // while chunk i's column results are still in the Infinity Cache
-    if (L.variant == 3 && (log2m == 15 || log2m == 16))
+    // The fused one-workgroup-per-window form (fused_kernel, 512 threads, no register prefetch) is the default
+    // for fp64 N = 65536, the legacy default window (4096 x 65536: 1.387 ms against 1.444 for the two-pass form,
+    // profiles/r03/s2); N = 131072 would hold 192 slots of 1 MiB at most (a quarter of the CUs idle) and stays
+    // two-pass, like fp32 (unmeasured fused).  Ablations (wsp_plan_set_variant): 1 = two-pass forced, 2 = two-pass
+    // over quarter chunks on two internal streams, 3 = fused (N = 65536 / 131072), 4 = the 256-thread fused form
+    // with register prefetch (1.516 ms: one wave per SIMD cannot hide the FFT's latencies).
+    const bool fused_default = L.variant == 0 && log2m == 15 && sizeof(T) == 8;
+    if ((L.variant == 3 || fused_default) && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7, 512, false>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8, 512, false>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 4 && (log2m == 15 || log2m == 16))

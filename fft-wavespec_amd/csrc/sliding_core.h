@@ -39,6 +39,7 @@
 #include <atomic>
 
 #include "spectrum_core.h"  // topk_wave64: the one-wave top-k scan of the FFT kernel
+#include "wg_fft.h"        // the register-resident workgroup FFT of the top-k seeds
 #include "wsp_internal.h"
 
 namespace wsp {
@@ -335,6 +336,63 @@ __global__ __launch_bounds__(seed_nt<LOG2N>()) void slide_seed_kernel(SlideArgs 
         }
         if (m == 0 && t == 0) ws[NF * span] = d2{y[0].x, lvl};
     });
+}
+
+// The same seeds by the register-resident workgroup FFT (wg::wg_fft: N/16 threads, 16 points each, radix-16
+// Stockham passes with LDS only between passes -- 2 exchanges at N = 2048 / 4096 against 6 / 7 LDS round trips
+// of fft_lds at N/4 threads), one transform m at a time, every output in natural order to LDS and the band read
+// back: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}) as slide_seed_kernel (N >= 1024).
+template <int LOG2N, int NF, int DETREND>
+__global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideArgs a) {
+    using G = wg::LGeo<LOG2N>;
+    constexpr int N = 1 << LOG2N, M = N / 2, TP = G::TP, NM = (NF - 1) / 2, R = wg::last_radix<LOG2N>();
+    __shared__ core::cpx<double> lds[G::SLOT];
+    const int t = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    if (w0 >= a.n_windows) return;
+    const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
+    const core::cpx<double> *__restrict__ tw = static_cast<const core::cpx<double> *>(a.twiddle);
+    const d2 *__restrict__ mod = static_cast<const d2 *>(a.omega) + (NF + 1) * M;  // [NM][N] e^{-j m th i}
+    const double lvl = DETREND == kDetrendMean ? x[0] : 0.0;
+    d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int span = a.span, kmin = a.kmin;
+    double xs[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xs[r] = x[t + TP * r] - lvl;
+#pragma unroll
+    for (int m = 0; m <= NM; ++m) {
+        core::cpx<double> v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (m == 0) {
+                v[r] = core::cpx<double>{xs[r], 0.0};
+            } else {
+                const d2 e = mod[(m - 1) * N + t + TP * r];
+                v[r] = core::cpx<double>{xs[r] * e.x, xs[r] * e.y};
+            }
+        }
+        wg::wg_fft<double, LOG2N>(v, lds, t, tw, LOG2N);  // ends after a barrier: lds is free
+        // v[q R + r] = Y[b + (N/R) r], b = t + TP q: natural order into lds
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) lds[core::pad16(t + TP * q + (N / R) * r)] = v[q * R + r];
+        __syncthreads();
+        const double s = m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2);
+        for (int j = t; j < span; j += TP) {
+            const int k = kmin + j;
+            const core::cpx<double> yp = lds[core::pad16(k)];
+            if (m == 0) {
+                ws[j] = s * d2{yp.re, yp.im};
+            } else {
+                const core::cpx<double> ym = lds[core::pad16((N - k) & (N - 1))];
+                ws[(2 * m - 1) * span + j] = s * d2{yp.re, yp.im};
+                ws[(2 * m) * span + j] = s * d2{ym.re, -ym.im};
+            }
+        }
+        if (m == 0 && t == 0) ws[NF * span] = d2{lds[0].re, lvl};  // sum of x - L (mean path), L
+        __syncthreads();  // the band reads before the next transform's exchanges
+    }
 }
 
 // One wave per segment: lane l tracks bins kmin + l + 64 b (b < NB), stages each window's band X in LDS
@@ -771,8 +829,12 @@ __global__ __launch_bounds__(64) void slide_topk_p_kernel(SlideArgs a) {
 
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
-    hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0, s,
-                       a);
+    if constexpr (LOG2N >= 10) {
+        hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3((1 << LOG2N) / 16), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0,
+                           s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int nb = (a.span + 63) / 64;

@@ -318,7 +318,7 @@ class Plan:
         _check("wsp_plan_set_slide_segment", lib().wsp_plan_set_slide_segment(self.handle, windows))
 
     def set_variant(self, variant: int) -> None:
-        """Ablation: the hop = 1 top-k scan form (0 auto, 1 one-wave, 2 / 3 transposed 16 / 8 windows)."""
+        """Ablation: the kernel form (include/mtbridge.h wsp_plan_set_variant; 0 = the library's choice)."""
         _check("wsp_plan_set_variant", lib().wsp_plan_set_variant(self.handle, variant))
 
     def algorithm(self) -> str:

@@ -298,10 +298,18 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
-/* Tuning / ablation: the form of the hop = 1 top-k scan by the sliding DFT.
- * 0 = the library's choice (default); 1 = one wave-wide reduction round per
- * slot and window; 2 / 3 = the transposed lane-per-window scan (k <= 8, bands
- * <= 256 bins) staging 16 / 8 windows per batch.  Same records either way. */
+/* Tuning / ablation: the kernel form, 0..5 (MTB_BAD_ARGS outside); 0 = the
+ * library's choice (default).  Same records within the parity bars either way.
+ *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
+ *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
+ *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch (0: the
+ *    probe-threshold scan);
+ *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
+ *    windows; 2 = the same pipelined over two internal streams; 3 = the fused
+ *    one-workgroup-per-window kernel (N = 65536 / 131072; the default for fp64
+ *    N = 65536); 4 = its 256-thread form with register prefetch;
+ *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
+ *    one-lane-per-window filter. */
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);

@@ -3,18 +3,19 @@
 #   1) --kernel-trace --stats      (per-kernel durations)
 #   2) --pmc FETCH_SIZE            (own pass; HBM read bytes, x2 gfx950 correction)
 #   3) --pmc WRITE_SIZE            (own pass)
-# Usage: bash scripts/gpu_profile.sh <tag> [config] [algo: auto|fft|slide]
+# Usage: bash scripts/gpu_profile.sh <tag> [config] [algo: auto|fft|slide] [variant]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-TAG=$1; CFG=${2:-north_star}; ALGO=${3:-auto}
+TAG=$1; CFG=${2:-north_star}; ALGO=${3:-auto}; VAR=${4:-0}
 KEY=$CFG; [ "$ALGO" = auto ] || KEY=${CFG}_$ALGO
+[ "$VAR" = 0 ] || KEY=${KEY}_v$VAR
 OUT=gpurun_out/prof_${TAG}_${KEY}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py --config $CFG --steps 100 --warmup 20 --no-cpu-baseline --algo $ALGO > $OUT/trace.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 100 --warmup 20 --no-cpu-baseline --algo $ALGO --variant $VAR > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
-  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO > $OUT/fetch.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO --variant $VAR > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
-  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO > $OUT/write.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --algo $ALGO --variant $VAR > $OUT/write.log 2>&1 || exit $?
 python3 scripts/parse_prof.py $OUT $CFG $KEY

@@ -14,9 +14,10 @@ from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
 key = sys.argv[3] if len(sys.argv) > 3 else cfg  # e.g. c4_fft: the config under a forced algorithm
-OURS = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_seed_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
+OURS = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "slide_seed_kernel", "slide_seed_r_kernel", "fused_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
         "iir_kernel")
-MAIN = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "inverse_kernel", "row_kernel")  # one per step; a Kalman pre-pass adds to its step
+MAIN = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "inverse_kernel", "row_kernel",
+        "fused_kernel")  # one per step; a Kalman pre-pass adds to its step
 
 
 def rows(pattern):
@@ -42,6 +43,8 @@ def main_per_step(cfg):
     c = synth.CONFIGS.get(cfg)
     if not c or c["n"] <= 16384:
         return 1
+    if c["n"] == 65536 and c["precision"] == "f64" and not key.endswith(("_v1", "_v2", "_v4")):
+        return 1  # the fused kernel: one launch over every window (large_fft.hip)
     per = (c["n"] // 2) * (8 if c["precision"] == "f32" else 16)
     chunk = max(1, (192 << 20) // per)
     return -(-c["windows"] // chunk)

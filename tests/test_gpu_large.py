@@ -130,12 +130,17 @@ def test_large_device_plan(gpu_session):
 
 
 @pytest.mark.parametrize("n,variant,detrend,window,output", [
+    (65536, 0, "none", "hann", "power"), (65536, 0, "mean", "bartlett", "packed"), (65536, 0, "iir", "hamming", "power"),
     (65536, 2, "none", "hann", "power"), (65536, 3, "none", "hann", "power"), (65536, 3, "mean", "blackman", "packed"),
-    (131072, 3, "none", "bartlett", "power"), (131072, 2, "iir", "hann", "power"), (32768, 2, "mean", "hamming", "power")])
+    (65536, 4, "none", "hann", "power"), (131072, 3, "none", "bartlett", "power"), (131072, 2, "iir", "hann", "power"),
+    (32768, 2, "mean", "hamming", "power")])
 def test_large_variants_identical(gpu_session, n, variant, detrend, window, output):
-    """The large-N ablation forms (wsp_plan_set_variant: 2 = two-pass over quarter chunks pipelined on two
-    internal streams, 3 = the fused one-workgroup-per-window kernel) run the same arithmetic as the default
-    two-pass form: identical records (variant 2) or within 1e-13 (variant 3), and the oracle's bar."""
+    """The large-N kernel forms (wsp_plan_set_variant) against the two-pass form (variant 1): 0 = the library's
+    choice (the fused kernel for fp64 N = 65536), 2 = two-pass over quarter chunks pipelined on two internal
+    streams, 3 = the fused one-workgroup-per-window kernel at 512 threads, 4 = the same at 256 threads with
+    register prefetch.  They run the same arithmetic: identical records (variant 2) or within 1e-13 (the fused
+    kernel: the same operations, contracted differently by the compiler; its window angles by rotation across
+    column blocks), and the oracle's bar."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     nwin = 37
@@ -143,7 +148,7 @@ def test_large_variants_identical(gpu_session, n, variant, detrend, window, outp
     d_s = torch.from_numpy(s).to(dev)
     period = 1024 if detrend == "iir" else 0
     outs = []
-    for v in (0, variant):
+    for v in (1, variant):
         plan = bridge.Plan(0, n, n, nwin, detrend, window, period, "f64", output)
         plan.set_variant(v)
         o = torch.empty(nwin * plan.record, dtype=torch.float64, device=dev)
@@ -153,8 +158,28 @@ def test_large_variants_identical(gpu_session, n, variant, detrend, window, outp
         plan.close()
     if variant == 2:  # the same kernels over other chunk boundaries: identical
         assert np.array_equal(outs[0], outs[1])
-    else:  # the fused kernel: the same operations, contracted differently by the compiler
+    else:
         den = np.abs(outs[0]).max(axis=1, keepdims=True)
         assert np.max(np.abs(outs[1] - outs[0]) / den) <= 1e-13
     if output == "power":
         assert oracle.rel_err(outs[1][:4], ref(s[:4 * n], n, n, detrend, window, period)) <= TOL["f64"]
+
+
+def test_large_fused_more_windows_than_slots(gpu_session):
+    """The default fused kernel (fp64, N = 65536) walks windows g, g + grid, ... over its slots: a batch of
+    more windows than workgroups (600 > 256 CUs) with a ragged tail, against the oracle on sampled windows."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 65536, 600
+    s = synth.random_walk(nwin * 4096 + n, seed=21)
+    plan = bridge.Plan(0, n, 4096, nwin, "none", "hann")
+    try:
+        d_s = torch.from_numpy(s).cuda()
+        d_o = torch.empty(nwin * (n // 2), dtype=torch.float64, device="cuda")
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        p = d_o.cpu().numpy().reshape(nwin, n // 2)
+    finally:
+        plan.close()
+    for w in (0, 255, 256, 511, 599):
+        r = ref(s[w * 4096:w * 4096 + n], n, n)
+        assert oracle.rel_err(p[w:w + 1], r) <= TOL["f64"], w
