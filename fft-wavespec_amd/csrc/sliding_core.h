@@ -211,7 +211,7 @@ __device__ __forceinline__ SlideSeg slide_seg_of(const SlideGroup &g, int64_t se
 
 template <typename T, int LOG2N, int NF, int DETREND>
 __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
-                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? 3 : 4))) void slide_kernel(SlideArgs a,
+                             slide_b<LOG2N>() == 2 ? 4 : (NF >= 5 ? 2 : (NF >= 3 ? (LOG2N == 12 && DETREND == kDetrendNone ? 4 : 3) : 4))) void slide_kernel(SlideArgs a,
                                                                                                               SlideGroup g) {
     constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B;
     constexpr int REC = Rec<NF>::n;
@@ -541,16 +541,10 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
                 for (int f = 1; f < NF; ++f) X += tr[b][f];
                 if constexpr (DETREND == kDetrendMean) X -= mwv * hk[b];
                 const int j = l + 64 * b;
-#ifdef WSP_TOPK_ABLATION
-                if (a.variant == 5) continue;  // timing ablation: slide only
-#endif
                 if (j < span) xs[slot * sp + j] = X;
             }
             if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
             if (slot != WB - 1 && wi + 1 < len) continue;
-#ifdef WSP_TOPK_ABLATION
-            if (a.variant >= 4) continue;  // timing ablation: no scan, no records
-#endif
             // ---- scan the staged batch: windows wi - slot .. wi
             __syncthreads();
             const bool wok = mw <= slot;
@@ -686,11 +680,13 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
 // reference's k-slot insertion (strict '>', gpuopt-nodetrend.mq5:545-552) over its list only.  A window
 // with more than kPCand candidates, or the segment's first, is scanned exactly by the one-wave reduction
 // (core::topk_wave64), whose winners then probe that slot.
-constexpr int kPCand = 16;  // candidate list entries per window
+constexpr int kPCand = 16;  // candidate list entries per window (default form)
 
-template <int LOG2N, int NF, int DETREND, int NB, int WB>
-__global__ __launch_bounds__(64) void slide_topk_p_kernel(SlideArgs a) {
-    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, CHT = 128, K = kTopkT, C = kPCand;
+// The LDS a wave holds sets the occupancy (one wave per workgroup): WB windows per batch x C candidates
+// (20 B each) + CHT staged steps of uniforms + the fallback's band.
+template <int LOG2N, int NF, int DETREND, int NB, int WB, int C = 16, int CHT = 128, int LB = 1>
+__global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_kernel(SlideArgs a) {
+    constexpr int N = 1 << LOG2N, M = N / 2, REC = Rec<NF>::n, K = kTopkT;
     constexpr int kEmpty = 0x7fffffff;
     static_assert(WB <= 32 && CHT % WB == 0, "one lane and one mask bit per window of a batch");
     __shared__ double u[CHT * REC];
@@ -843,12 +839,22 @@ template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideAr
     // staged batch (4 lanes per window, 2 merge rounds) while the batch takes <= 16 KiB of LDS, else 8
     // (variant 2 / 3 force 16 / 8: ablations)
     const size_t row = (size_t)(a.span | 1) * 2 * sizeof(double);
-    const int wb = (a.variant == 2 || a.variant >= 4) ? 16 : (a.variant == 3 ? 8 : (16 * row <= (16u << 10) ? 16 : 8));
+    const int wb = a.variant == 2 ? 16 : (a.variant == 3 ? 8 : (16 * row <= (16u << 10) ? 16 : 8));
     static_assert(kCand >= 1, "candidate list");
-    if (a.topk <= kTopkT && a.variant == 0 && nb <= 4) {  // probe threshold, 32 windows per batch
-        if (nb <= 1) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 1, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
-        else if (nb <= 2) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 2, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 4, 32>), dim3((unsigned)grid), dim3(64), 0, s, a);
+    if (a.topk <= kTopkT && (a.variant == 0 || a.variant >= 4) && nb <= 4) {  // probe threshold
+#define PROBE(...)                                                                                                       \
+    do {                                                                                                                 \
+        if (nb <= 1) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 1, __VA_ARGS__>), dim3((unsigned)grid), dim3(64), 0, s, a); \
+        else if (nb <= 2) hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 2, __VA_ARGS__>), dim3((unsigned)grid), dim3(64), 0, s, a); \
+        else hipLaunchKernelGGL((slide_topk_p_kernel<LOG2N, NF, DETREND, 4, __VA_ARGS__>), dim3((unsigned)grid), dim3(64), 0, s, a); \
+    } while (0)
+        // the LDS per wave sets the occupancy: 16 windows per batch x 16 candidates + 64 staged steps = 9.8 KiB and
+        // <= 128 VGPRs: 4 waves per SIMD (C4 top-8 0.389 ms; 32 windows x 16 candidates + 128 steps = 17 KiB:
+        // 2.25 waves per SIMD, 0.449 ms; 32 x 12 + 64 steps = 12 KiB: 3 waves, 0.433 ms -- profiles/r03/s2)
+        if (a.variant == 4) PROBE(32, kPCand, 128, 1);
+        else if (a.variant == 5) PROBE(32, 12, 64, 3);
+        else PROBE(16, kPCand, 64, 4);
+#undef PROBE
         return hipGetLastError();
     }
     if (a.topk <= kTopkT && a.variant != 1 && nb <= 4) {
@@ -908,8 +914,8 @@ hipError_t launch_t(const SlideArgs &a0, const SlideGroup &g0, hipStream_t s) {
     SlideGroup g = g0;
     int64_t total = 0;
     for (int m = 0; m < g.n; ++m) total += g.n_windows[m];
-    if (a.seg <= 0) {  // ~2 rounds of resident workgroups, 32..256 windows each (sweep: DESIGN.md 4.5)
-        a.seg = (total + 2 * (int64_t)res - 1) / (2 * (int64_t)res);
+    if (a.seg <= 0) {  // one round of resident workgroups, 32..256 windows each (sweeps: DESIGN.md 4.5)
+        a.seg = (total + (int64_t)res - 1) / (int64_t)res;
         a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
     }
     g.blk0[0] = 0;

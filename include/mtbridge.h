@@ -302,8 +302,9 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
- *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch (0: the
- *    probe-threshold scan);
+ *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch; 0 = the
+ *    probe-threshold scan (16 windows per batch, 4 waves per SIMD), 4 / 5 = the
+ *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams; 3 = the fused
  *    one-workgroup-per-window kernel (N = 65536 / 131072; the default for fp64

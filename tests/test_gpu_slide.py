@@ -239,6 +239,34 @@ def test_slide_topk_slots_and_bands(gpu_session, k, pmin, pmax):
     _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=8 if k == 64 else 2)
 
 
+@pytest.mark.parametrize("n,pmin,pmax,seg", [(2048, 18.0, 200.0, 0), (2048, 18.0, 200.0, 100), (1024, 5.0, 200.0, 0),
+                                             (4096, 18.0, 200.0, 70), (2048, 10.0, 2000.0, 0)])
+def test_slide_topk_scan_forms_identical(gpu_session, n, pmin, pmax, seg):
+    """Every form of the hop = 1 top-k scan (wsp_plan_set_variant: 0 probe threshold, 1 one-wave reductions,
+    2 / 3 transposed 16 / 8 windows, 4 / 5 probe threshold with 32 windows x 16 candidates and 128 staged steps /
+    32 x 12 and 64; the default 16 x 16 and 64) takes the same decisions on the same tracker values: identical records, and the oracle's
+    bars.  Bands of 103 / 199 / 207 / 203 bins (two to four bins per lane)."""
+    torch = pytest.importorskip("torch")
+    nwin, k = 2500, 8
+    s = synth.random_walk(nwin + n - 1, seed=n + seg)
+    outs = []
+    for v in range(6):
+        plan = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+        plan.set_topk(k, pmin, pmax)
+        plan.set_algorithm("slide")
+        plan.set_variant(v)
+        if seg:
+            plan.set_slide_segment(seg)
+        outs.append(_run(plan, s, torch).reshape(nwin, k, 4))
+        plan.close()
+    for v in range(1, 6):
+        assert np.array_equal(outs[0], outs[v]), v
+    want = oracle.batch_topk(s, n, 1, "none", "hann", 0, None, k, pmin, pmax)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = int(np.ceil(n / pmax)), min(int(np.floor(n / pmin)), n // 2 - 1)
+    _topk_bars(outs[0], want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
 def test_slide_topk_vs_fft_c4(gpu_session):
     """C4's batch (1,048,576 windows x 2048) as top-8 records: sliding DFT against the FFT kernel's fused
     scan on the same device buffer, every window."""
