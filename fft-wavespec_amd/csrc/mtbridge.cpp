@@ -338,7 +338,23 @@ struct WsLayout {
 };
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 bool use_slide_topk(const Config &c);
-int64_t slide_topk_seg(const Config &c) { return c.slide_seg > 0 ? c.slide_seg : 128; }  // swept 32..256: 128 best
+// Windows per top-k segment: whole rounds of resident one-wave workgroups (the default probe scan runs 4 per
+// SIMD = 16 per CU) at <= 256 windows each -- C4 (1,048,576 windows): one round of 4096 segments of 256,
+// 0.371-0.374 ms against 0.389 for 128-window segments (two rounds) and 0.41 / 0.50 for 192 / 384
+// (1.33 rounds / a quarter of the slots idle; profiles/r03/s2/topk_seg.log).  At least 64 windows.
+int64_t slide_topk_seg(const Config &c) {
+    if (c.slide_seg > 0) return c.slide_seg;
+    static const int64_t res = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        return (int64_t)16 * cus;
+    }();
+    const int64_t rounds = (c.n_windows + res * 256 - 1) / (res * 256);
+    const int64_t seg = (c.n_windows + res * rounds - 1) / (res * rounds);
+    return seg < 64 ? 64 : seg;
+}
 WsLayout ws_layout(const Config &c) {
     WsLayout L;
     if (use_slide_topk(c)) {

@@ -136,6 +136,15 @@ hipError_t hipSetDevice(int d) {
     t_device = d;
     return hipSuccess;
 }
+hipError_t hipGetDevice(int *d) {
+    *d = t_device;
+    return hipSuccess;
+}
+hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t attr, int d) {
+    if (d < 0 || d >= n_devices()) return hipErrorInvalidDevice;
+    *v = attr == hipDeviceAttributeMultiprocessorCount ? 256 : 0;  // an MI355X's CUs; nothing else is asked
+    return hipSuccess;
+}
 hipError_t hipMalloc(void **p, size_t n) {
     *p = aligned_alloc(256, (n + 255) & ~size_t(255));
     if (!*p) return hipErrorOutOfMemory;
