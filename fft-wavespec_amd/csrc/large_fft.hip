@@ -272,7 +272,8 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
-template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true>
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true,
+          bool NTS = false>
 __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
@@ -447,7 +448,11 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 const int il = sl < RB ? sl : sl - RB, l2 = beta2 * RB + il;
                 const int64_t k = (sl < RB ? l2 : (l2 == 0 ? M2 / 2 : M2 - l2)) + (int64_t)M2 * k1;
 #pragma unroll
-                for (int e = 0; e < E; ++e) ow[k * E + e] = stage[(k1 * (2 * RB + 1) + sl) * E + e];
+                for (int e = 0; e < E; ++e) {
+                    const T o = stage[(k1 * (2 * RB + 1) + sl) * E + e];
+                    if constexpr (NTS) __builtin_nontemporal_store(o, ow + k * E + e);  // keep the slots in the MALL
+                    else ow[k * E + e] = o;
+                }
             }
             __syncthreads();
         }
@@ -593,7 +598,7 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
 
 // the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablations: variant 3 =
 // 512 threads without register prefetch, two waves per SIMD; variant 4 = 256 threads with prefetch)
-template <typename T, int LM1, int NT, bool PF>
+template <typename T, int LM1, int NT, bool PF, bool NTS = false>
 hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const large::RowArgs &ra, int wclass, bool mean,
                         hipStream_t s) {
     large::ColArgs ca = ca0;
@@ -606,11 +611,11 @@ hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const l
     using namespace core;
 #define FUSED(WC)                                                                                                          \
     if (mean) {                                                                                                            \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     } else {                                                                                                               \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     }
     switch (wclass) {
     case kWinCos: FUSED(kWinCos); break;
@@ -734,9 +739,13 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     // over quarter chunks on two internal streams, 3 = fused (N = 65536 / 131072), 4 = the 256-thread fused form
     // with register prefetch (1.516 ms: one wave per SIMD cannot hide the FFT's latencies).
     const bool fused_default = L.variant == 0 && log2m == 15 && sizeof(T) == 8;
+    // (non-temporal output stores: the streamed spectra do not evict the slots from the Infinity Cache --
+    // 1.376 -> 1.346 ms; variant 5 keeps plain stores)
     if ((L.variant == 3 || fused_default) && (log2m == 15 || log2m == 16))
-        return log2m == 15 ? fused_launch<T, 7, 512, false>(L, ca, ra, wclass, means != nullptr, s)
-                           : fused_launch<T, 8, 512, false>(L, ca, ra, wclass, means != nullptr, s);
+        return log2m == 15 ? fused_launch<T, 7, 512, false, true>(L, ca, ra, wclass, means != nullptr, s)
+                           : fused_launch<T, 8, 512, false, true>(L, ca, ra, wclass, means != nullptr, s);
+    if (L.variant == 5 && log2m == 15)  // ablation: the fused form with plain output stores
+        return fused_launch<T, 7, 512, false, false>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 4 && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7, 256, true>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8, 256, true>(L, ca, ra, wclass, means != nullptr, s);

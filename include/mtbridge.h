@@ -308,7 +308,8 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams; 3 = the fused
  *    one-workgroup-per-window kernel (N = 65536 / 131072; the default for fp64
- *    N = 65536); 4 = its 256-thread form with register prefetch;
+ *    N = 65536); 4 = its 256-thread form with register prefetch; 5 = the fused
+ *    kernel with plain (not non-temporal) output stores;
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter. */
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);

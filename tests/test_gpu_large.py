@@ -132,15 +132,16 @@ def test_large_device_plan(gpu_session):
 @pytest.mark.parametrize("n,variant,detrend,window,output", [
     (65536, 0, "none", "hann", "power"), (65536, 0, "mean", "bartlett", "packed"), (65536, 0, "iir", "hamming", "power"),
     (65536, 2, "none", "hann", "power"), (65536, 3, "none", "hann", "power"), (65536, 3, "mean", "blackman", "packed"),
-    (65536, 4, "none", "hann", "power"), (131072, 3, "none", "bartlett", "power"), (131072, 2, "iir", "hann", "power"),
+    (65536, 4, "none", "hann", "power"), (65536, 5, "mean", "hann", "power"), (131072, 3, "none", "bartlett", "power"),
+    (131072, 2, "iir", "hann", "power"),
     (32768, 2, "mean", "hamming", "power")])
 def test_large_variants_identical(gpu_session, n, variant, detrend, window, output):
     """The large-N kernel forms (wsp_plan_set_variant) against the two-pass form (variant 1): 0 = the library's
     choice (the fused kernel for fp64 N = 65536), 2 = two-pass over quarter chunks pipelined on two internal
     streams, 3 = the fused one-workgroup-per-window kernel at 512 threads, 4 = the same at 256 threads with
-    register prefetch.  They run the same arithmetic: identical records (variant 2) or within 1e-13 (the fused
-    kernel: the same operations, contracted differently by the compiler; its window angles by rotation across
-    column blocks), and the oracle's bar."""
+    register prefetch, 5 = the fused kernel with plain output stores.  They run the same arithmetic: identical
+    records (variant 2) or within 1e-13 (the fused kernel: the same operations, contracted differently by the
+    compiler; its window angles by rotation across column blocks), and the oracle's bar."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     nwin = 37
