@@ -734,6 +734,11 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
 #pragma unroll 1
         for (int st = 0; st < clen; ++st) {
             const int wi = c0 + st, slot = wi % WB;
+            // this step's uniforms into registers first: the LDS latency then overlaps the window's scan instead of
+            // sitting in front of the slide (the last window's are never used)
+            double ur[REC];
+#pragma unroll
+            for (int i = 0; i < REC; ++i) ur[i] = u[st * REC + i];
             const double mwv = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
             d2 X[NB];
             int ph[NB];  // high words of the powers (non-negative doubles order as their bits); INT_MIN outside
@@ -784,7 +789,7 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
                     for (int b = 0; b < NB; ++b) mask[b] = nm[l + 64 * b] ? 0xffffffffu : 0u;
                 }
             }
-            if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, u + st * REC, sum);
+            if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, ur, sum);
             if (slot != WB - 1 && wi + 1 < len) continue;
             // ---- the staged batch, one lane per window: windows wi - slot .. wi
             __syncthreads();
