@@ -484,6 +484,42 @@ template <int K> __device__ __forceinline__ void topk_insert(double (&tp)[K], in
     tp[0] = c[0] ? p : tp[0];
     tb[0] = c[0] ? j : tb[0];
 }
+// Merge the LPW sorted partial lists (power desc, index asc) of a window held by lanes mw + WB q: log2 LPW
+// rounds of exchange with the partner lane, each keeping the best K of the two lists by a bitonic merge
+// (best of mine[s] and the partner's [K-1-s] is the union's top K in bitonic order; half-cleaners sort it).
+// Every lane of the window ends with the same sorted top K.
+template <int K, int WB, int LPW> __device__ __forceinline__ void merge_parts(double (&tp)[K], int (&tb)[K]) {
+#pragma unroll
+    for (int r = 1; r < LPW; r <<= 1) {
+        double op[K];
+        int ob[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            op[s] = __shfl_xor(tp[s], WB * r, 64);
+            ob[s] = __shfl_xor(tb[s], WB * r, 64);
+        }
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            const bool t = kbetter(op[K - 1 - s], ob[K - 1 - s], tp[s], tb[s]);
+            tp[s] = t ? op[K - 1 - s] : tp[s];
+            tb[s] = t ? ob[K - 1 - s] : tb[s];
+        }
+#pragma unroll
+        for (int h = K / 2; h > 0; h >>= 1)
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if ((i & h) == 0) {
+                    const bool t = kbetter(tp[i + h], tb[i + h], tp[i], tb[i]);
+                    const double pa = tp[i], pb = tp[i + h];
+                    const int ba = tb[i], bb = tb[i + h];
+                    tp[i] = t ? pb : pa;
+                    tp[i + h] = t ? pa : pb;
+                    tb[i] = t ? bb : ba;
+                    tb[i + h] = t ? ba : bb;
+                }
+    }
+}
+
 constexpr int kCand = 8;  // candidate list entries per lane of the transposed scan (+1 scratch slot)
 
 template <int LOG2N, int NF, int DETREND, int NB, int WB>
@@ -603,38 +639,7 @@ __global__ __launch_bounds__(64) void slide_topk_t_kernel(SlideArgs a) {
                     for (int i = 0; i < 4; ++i) topk_insert<K>(tp, tb, pw[i], j + i * LPW);
                 }
             }
-            // merge the LPW partial lists of a window (lanes mw + WB q): keep the best 8 of each pair
-#pragma unroll
-            for (int r = 1; r < LPW; r <<= 1) {
-                double op[K];
-                int ob[K];
-#pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    op[s] = __shfl_xor(tp[s], WB * r, 64);
-                    ob[s] = __shfl_xor(tb[s], WB * r, 64);
-                }
-                // best of mine[s] and the partner's [K-1-s]: the 8 best of the union, in bitonic order
-#pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    const bool t = kbetter(op[K - 1 - s], ob[K - 1 - s], tp[s], tb[s]);
-                    tp[s] = t ? op[K - 1 - s] : tp[s];
-                    tb[s] = t ? ob[K - 1 - s] : tb[s];
-                }
-                // bitonic half-cleaners: best first
-#pragma unroll
-                for (int h = K / 2; h > 0; h >>= 1)
-#pragma unroll
-                    for (int i = 0; i < K; ++i)
-                        if ((i & h) == 0) {
-                            const bool t = kbetter(tp[i + h], tb[i + h], tp[i], tb[i]);
-                            const double pa = tp[i], pb = tp[i + h];
-                            const int ba = tb[i], bb = tb[i + h];
-                            tp[i] = t ? pb : pa;
-                            tp[i + h] = t ? pa : pb;
-                            tb[i] = t ? bb : ba;
-                            tb[i + h] = t ? ba : bb;
-                        }
-            }
+            merge_parts<K, WB, LPW>(tp, tb);  // the LPW partial lists of a window (lanes mw + WB q)
 #pragma unroll
             for (int s = 0; s < K; ++s) pb[s] = tb[s];  // this slot's winners: the next batch's threshold bins
             have_prev = true;
@@ -791,30 +796,34 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
             }
             if (wi + 1 < len) slide_step<NB, NF, DETREND>(tr, om, ur, sum);
             if (slot != WB - 1 && wi + 1 < len) continue;
-            // ---- the staged batch, one lane per window: windows wi - slot .. wi
+            // ---- the staged batch: windows wi - slot .. wi, LPW = 64 / WB lanes per window (lane l: window
+            // mw = l % WB, candidates q, q + LPW, ... of it, q = l / WB), merged across the window's lanes
             __syncthreads();
-            const int n = l <= slot ? cnt[l] : -1;
+            constexpr int LPW = 64 / WB;
+            const int mw = l % WB, q = l / WB;
+            const int n = mw <= slot ? cnt[mw] : -1;
             double tp[K];
             int tb[K];
 #pragma unroll
             for (int s = 0; s < K; ++s) tp[s] = -1.0, tb[s] = kEmpty;
-            for (int i = 0; __ballot(i < n) != 0; ++i) {
+            for (int i = q; __ballot(i < n) != 0; i += LPW) {
                 const bool on = i < n;
-                const d2 v = cx[l * C + (on ? i : 0)];
+                const d2 v = cx[mw * C + (on ? i : 0)];
                 topk_insert<K>(tp, tb, on ? v.x * v.x + v.y * v.y : -1.0, on ? i : kEmpty);  // i: ascending bins
             }
-            if (n >= 0) {
-                double *o = rec + (int64_t)(wi - slot + l) * (4 * kk);
+            merge_parts<K, WB, LPW>(tp, tb);  // (power desc, index asc): the sequential insertion's order
+            if (n >= 0 && q == 0) {
+                double *o = rec + (int64_t)(wi - slot + mw) * (4 * kk);
                 typedef double d4 __attribute__((ext_vector_type(4)));
 #pragma unroll
                 for (int s = 0; s < K; ++s) {
                     if (s < kk) {
                         const bool real = tb[s] != kEmpty;
-                        const int ci = real ? l * C + tb[s] : 0;
+                        const int ci = real ? mw * C + tb[s] : 0;
                         const d2 v = cx[ci];
                         const int bj = cb[ci];
                         *reinterpret_cast<d4 *>(o + 4 * s) = real ? d4{(double)(kmin + bj), tp[s], v.x, v.y} : d4{-1.0, -1.0, 0.0, 0.0};
-                        if (real) atomicOr(&nm[bj], 1u << l);
+                        if (real) atomicOr(&nm[bj], 1u << mw);
                     }
                 }
             }
