@@ -67,8 +67,9 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=0, help="kernel form (wsp_plan_set_variant; ablations)")
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
                     help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
-    ap.add_argument("--c5-streams", type=int, default=1,
-                    help="C5: streams the grouped plan forks over (wsp_group_set_streams) / the symbol plans use")
+    ap.add_argument("--c5-streams", type=int, default=0,
+                    help="C5: lanes the grouped plan runs its launches on (wsp_group_set_streams; 0 = the library's "
+                         "default, one per window length up to 4) / streams the symbol plans use (0 = 3)")
     ap.add_argument("--c5-mode", default="group", choices=["group", "plans"],
                     help="C5: one grouped device plan (wsp_group_*: one launch per window length) or one plan per "
                          "symbol spread over --c5-streams streams (round-2 form, ablation)")
@@ -380,13 +381,13 @@ class C5Batch(Workload):
             self.outs = [torch.empty(nwins[sym] * (lens[sym // 7] // 2), dtype=torch.float64, device=dev)
                          for sym in owned]
             self.group = bridge.Group(local_rank, [lens[sym // 7] for sym in owned], [nwins[sym] for sym in owned])
-            if c5_streams != 1:
+            if c5_streams:
                 self.group.set_streams(c5_streams)
             if slide_seg:
                 self.group.set_segment(slide_seg)
             self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
             self.algorithm = "slide-group"
-            self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams,
+            self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams or "library default",
                            "segment": slide_seg or "auto"}
             self.windows = sum(nwins[sym] for sym in owned)
             self.alg_bytes = self.group.algorithmic_bytes
@@ -403,7 +404,7 @@ class C5Batch(Workload):
         # stream by output bytes (what the hop = 1 sliding DFT's time follows: nwin x N/2), "nlogn" the
         # same by windows x N log N (the FFT kernel's work).  --c5-streams 1 runs every symbol on one
         # stream (ablation).
-        nstreams = c5_streams
+        nstreams = c5_streams or 3
         self.streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
         if c5_layout == "nlogn":
             cost = {sym: nwins[sym] * lens[sym // 7] * int(np.log2(lens[sym // 7])) for sym in owned}

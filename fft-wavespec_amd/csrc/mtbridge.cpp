@@ -1100,10 +1100,9 @@ struct Group {
     std::vector<int64_t> launch_bytes;     // output bytes per launch: what the slide's time follows
     std::mutex mu;                         // executes on the internal streams are enqueued one at a time
     int64_t seg = 0;                       // windows per workgroup, 0 = the launcher's policy
-    // wsp_group_set_streams(n > 1): the launches fork from the caller's stream onto n internal streams
-    // (greedy by output bytes, longest first) and join back, so that one length's tail overlaps the next
+    // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
     std::vector<hipStream_t> streams;
-    std::vector<hipEvent_t> events;  // [0] fork, [1 + i] join of stream i
+    std::vector<hipEvent_t> events;  // [0] fork, [k] join of internal stream k - 1
     void release() {
         (void)hipSetDevice(dev);
         for (auto st : streams) {
@@ -1124,6 +1123,33 @@ std::shared_ptr<Group> find_group(int64_t id) {
     auto it = g_groups->find(id);
     return it == g_groups->end() ? nullptr : it->second;
 }
+
+// (under g.mu) n lanes for wsp_group_execute: the caller's stream + n - 1 internal streams and their events
+int group_lanes(Group &g, int n_streams) {
+    g.release();
+    if (n_streams == 1) return MTB_OK;
+    HIP_OR(hipSetDevice(g.dev), MTB_BACKEND_UNAVAILABLE);
+    for (int i = 0; i < n_streams - 1; ++i) {  // + the caller's stream = n_streams lanes
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+            g.release();
+            set_error("wsp_group_set_streams: stream creation failed");
+            return MTB_INTERNAL_ERROR;
+        }
+        g.streams.push_back(st);
+    }
+    for (int i = 0; i < n_streams; ++i) {  // [0] fork, [k] join of internal stream k
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            g.release();
+            set_error("wsp_group_set_streams: event creation failed");
+            return MTB_INTERNAL_ERROR;
+        }
+        g.events.push_back(e);
+    }
+    return MTB_OK;
+}
+
 
 }  // namespace
 
@@ -1800,6 +1826,13 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
             for (int m : g->launch.back()) b += g->cfg[m].n_windows * g->cfg[m].record() * (int64_t)g->cfg[m].elem();
             g->launch_bytes.push_back(b);
         }
+    // by default the launches run side by side, one lane each, up to 4 lanes (the HIP hardware queues a
+    // process gets): C5 0.705-0.709 -> 0.669-0.671 ms against one lane (profiles/r03/s2/c5_lanes.log)
+    {
+        std::lock_guard<std::mutex> glk(g->mu);
+        const int lanes = (int)std::min<size_t>(g->launch.size(), 4);
+        if (lanes > 1 && group_lanes(*g, lanes) != MTB_OK) return 0;
+    }
     const int64_t id = g_next_id.fetch_add(1);
     std::lock_guard<std::mutex> lk(g_groups_mu);
     (*g_groups)[id] = std::move(g);
@@ -1823,19 +1856,33 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
         }
     std::lock_guard<std::mutex> lk(g->mu);
     const hipStream_t caller = (hipStream_t)hip_stream;
-    const int ns = (int)g->streams.size();
+    // wsp_group_set_streams(n > 1): the launches run side by side on n lanes -- the caller's stream and n - 1
+    // internal streams (n HIP hardware queues in all) -- assigned greedily by output bytes, longest first, and
+    // each lane's launches sized for the lane's share of the resident workgroup slots (its bytes / all bytes),
+    // so that the lanes finish together and one length's seed phase and drain overlap the others' slides
+    const int ns = g->streams.empty() ? 1 : (int)g->streams.size();
     HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
+    std::vector<int> lane(g->launch.size(), 0);
+    std::vector<int64_t> load(ns, 0);
+    int64_t all = 0;
+    for (size_t li = 0; li < g->launch.size(); ++li) {  // longest windows first; greedy by output bytes
+        const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        lane[li] = k;
+        load[k] += g->launch_bytes[li];
+        all += g->launch_bytes[li];
+    }
+    auto lane_stream = [&](int k) { return k == 0 ? caller : g->streams[k - 1]; };
     if (ns > 1) {
         HIP_OR(hipEventRecord(g->events[0], caller), MTB_INTERNAL_ERROR);
-        for (auto st : g->streams) HIP_OR(hipStreamWaitEvent(st, g->events[0], 0), MTB_INTERNAL_ERROR);
+        for (int k = 1; k < ns; ++k) HIP_OR(hipStreamWaitEvent(lane_stream(k), g->events[0], 0), MTB_INTERNAL_ERROR);
     }
-    std::vector<int64_t> load(ns > 1 ? ns : 1, 0);
-    for (size_t li = 0; li < g->launch.size(); ++li) {  // longest windows first; greedy by output bytes
+    for (size_t li = 0; li < g->launch.size(); ++li) {
         const auto &L = g->launch[li];
         SlideArgs A{};
         const int st = slide_args(g->dev, g->cfg[L[0]], &A);
         if (st != MTB_OK) return st;
         A.seg = g->seg;
+        A.share = ns > 1 && load[lane[li]] > 0 ? (double)all / (double)load[lane[li]] : 1.0;
         SlideGroup G;
         G.n = (int)L.size();
         for (int i = 0; i < G.n; ++i) {
@@ -1843,14 +1890,12 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
             G.out[i] = d_out[L[i]];
             G.n_windows[i] = g->cfg[L[i]].n_windows;
         }
-        const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        load[k] += g->launch_bytes[li];
-        HIP_OR(launch_slide_group(A, G, ns > 1 ? g->streams[k] : caller), MTB_INTERNAL_ERROR);
+        HIP_OR(launch_slide_group(A, G, lane_stream(lane[li])), MTB_INTERNAL_ERROR);
     }
     if (ns > 1)
-        for (int i = 0; i < ns; ++i) {
-            HIP_OR(hipEventRecord(g->events[1 + i], g->streams[i]), MTB_INTERNAL_ERROR);
-            HIP_OR(hipStreamWaitEvent(caller, g->events[1 + i], 0), MTB_INTERNAL_ERROR);
+        for (int k = 1; k < ns; ++k) {
+            HIP_OR(hipEventRecord(g->events[k], lane_stream(k)), MTB_INTERNAL_ERROR);
+            HIP_OR(hipStreamWaitEvent(caller, g->events[k], 0), MTB_INTERNAL_ERROR);
         }
     return MTB_OK;
 }
@@ -1862,28 +1907,7 @@ MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams) {
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);
-    g->release();
-    if (n_streams == 1) return MTB_OK;
-    HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
-    for (int i = 0; i < n_streams; ++i) {
-        hipStream_t st = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-            g->release();
-            set_error("wsp_group_set_streams: stream creation failed");
-            return MTB_INTERNAL_ERROR;
-        }
-        g->streams.push_back(st);
-    }
-    for (int i = 0; i <= n_streams; ++i) {
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            g->release();
-            set_error("wsp_group_set_streams: event creation failed");
-            return MTB_INTERNAL_ERROR;
-        }
-        g->events.push_back(e);
-    }
-    return MTB_OK;
+    return group_lanes(*g, n_streams);
 }
 
 MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows) {

@@ -929,7 +929,8 @@ hipError_t launch_t(const SlideArgs &a0, const SlideGroup &g0, hipStream_t s) {
     int64_t total = 0;
     for (int m = 0; m < g.n; ++m) total += g.n_windows[m];
     if (a.seg <= 0) {  // one round of resident workgroups, 32..256 windows each (sweeps: DESIGN.md 4.5)
-        a.seg = (total + (int64_t)res - 1) / (int64_t)res;
+        const int64_t slots = a.share > 1.0 ? (int64_t)((double)res / a.share) + 1 : (int64_t)res;
+        a.seg = (total + slots - 1) / slots;
         a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
     }
     g.blk0[0] = 0;

@@ -124,6 +124,8 @@ struct SlideArgs {
     int kmin, span, topk;
     void *ws;             // ceil(n_windows / seg) * slide_topk_seed_stride(nf, span) double complex
     int variant;          // top-k scan: 0 = auto, 1 = one wave per window, 2 / 3 = transposed, 16 / 8 windows per batch
+    double share;         // launches running side by side (grouped plan on several streams): the launcher's
+                          // segments fill 1/share of the resident workgroup slots; 0 / 1 = all of them
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
 // Grouped launch: several series of the same window length (the symbols of one length in a

@@ -340,11 +340,12 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
 MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
 /* Kernel launches one execute makes (one per window length and 16 members). */
 MTB_API int32_t wsp_group_launches(int64_t group);
-/* Tuning: n_streams > 1 forks every execute from the caller's stream onto n
- * internal streams (launches assigned greedily by output bytes) and joins
- * them back into it (events; no host sync), so one window length's last
- * workgroups overlap the next length's first.  1 (default) = everything on
- * the caller's stream.  MTB_BAD_ARGS outside 1..8. */
+/* Tuning: n_streams > 1 runs every execute's launches side by side on n
+ * lanes -- the caller's stream and n - 1 internal streams forked from it and
+ * joined back (events; no host sync) -- assigned greedily by output bytes,
+ * each lane's launches sized for its share of the device's workgroup slots,
+ * so one window length's seed phase and last workgroups overlap the others'.
+ * 1 (default) = everything on the caller's stream.  MTB_BAD_ARGS outside 1..8. */
 MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams);
 /* Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy over
  * each window length's total window count), at most 2048. */

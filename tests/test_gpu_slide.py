@@ -402,6 +402,35 @@ def test_group_mixed_members(gpu_session, prec, detrend, window):
     g.close()
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 3, 8])
+def test_group_lanes(gpu_session, lanes):
+    """wsp_group_set_streams: the launches on 1 lane (the caller's stream), 2 / 3 lanes (several launches per lane)
+    or more lanes than launches (the default is one lane per launch, up to 4), each lane's launches sized for its
+    share of the workgroup slots: every window of every member against the oracle, and a second execute on the
+    same buffers (fork / join events reused) identical to the first."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    lens = [4096, 2048, 1024, 512, 2048, 512]
+    nwins = [900, 1500, 2100, 2600, 77, 3]
+    hs = [synth.random_walk(nw + n - 1, seed=300 + i) for i, (n, nw) in enumerate(zip(lens, nwins))]
+    series = [torch.from_numpy(h).to(dev) for h in hs]
+    outs = [torch.empty(nw * (n // 2), dtype=torch.float64, device=dev) for n, nw in zip(lens, nwins)]
+    g = bridge.Group(0, lens, nwins)
+    g.set_streams(lanes)
+    ptrs = ([x.data_ptr() for x in series], [o.data_ptr() for o in outs])
+    g.execute(*ptrs, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    first = [o.cpu().numpy().copy() for o in outs]
+    g.execute(*ptrs, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for i, (n, nw) in enumerate(zip(lens, nwins)):
+        got = outs[i].cpu().numpy()
+        assert np.array_equal(got, first[i]), i
+        want = oracle.batch_spectrum(hs[i], n, 1, "none", "hann")
+        assert oracle.rel_err(got.reshape(nw, n // 2), want) <= 1e-10, (i, n, nw)
+    g.close()
+
+
 def test_group_refusals(gpu_session):
     """Members the sliding DFT cannot take are refused at creation (no silent fallback)."""
     with pytest.raises(bridge.BridgeError):
