@@ -153,26 +153,34 @@ def timed_steps(step, sync, ctl: Control, steps: int, warmup: int, events=None) 
     return ctl.max(t1 - t0)
 
 
-def settle(step, stream, min_launches=8, max_ms=600.0, tol=0.03) -> dict:
-    """Repeat `step` until the last 8 launches' HIP-event durations agree within `tol` (or max_ms of
-    GPU time).  Untimed; returns what it did for the JSON line."""
+def settle(step, stream, batch=8, min_ms=150.0, max_ms=800.0, tol=0.02) -> dict:
+    """Untimed clock settle: the MI355X raises its memory clock only under sustained load, so run
+    `step` back to back in batches of `batch` launches (one HIP-event pair and one host sync per batch, no gap
+    between the launches of a batch) until at least `min_ms` of GPU time has passed and the last three batches'
+    per-launch times agree within `tol` (or `max_ms`).  Returns what it did for the JSON line."""
     import torch
-    durs = []
+    per = []
+    total = 0.0
+    n = 0
     t0 = time.perf_counter()
     while True:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        step()
+        for _ in range(batch):
+            step()
         b.record(stream)
         b.synchronize()
-        durs.append(a.elapsed_time(b))
-        last = durs[-min_launches:]
-        if len(durs) >= min_launches and max(last) <= (1 + tol) * min(last):
+        ms = a.elapsed_time(b)
+        total += ms
+        n += batch
+        per.append(ms / batch)
+        last = per[-3:]
+        if total >= min_ms and len(per) >= 3 and max(last) <= (1 + tol) * min(last):
             break
-        if sum(durs) >= max_ms:
+        if total >= max_ms:
             break
-    return {"launches": len(durs), "ms": round(sum(durs), 2), "first_ms": round(durs[0], 4),
-            "last_ms": round(durs[-1], 4), "wall_s": round(time.perf_counter() - t0, 3)}
+    return {"launches": n, "ms": round(total, 2), "first_ms": round(per[0], 4), "last_ms": round(per[-1], 4),
+            "wall_s": round(time.perf_counter() - t0, 3)}
 
 
 def cpu_model() -> str:
