@@ -112,3 +112,45 @@ def test_slide_model_level_shift_stress():
     kmin, kmax = oracle.band(n)
     assert oracle.rel_err(got, want) <= 1e-10
     assert oracle.inband_err(got, want, kmin, kmax) <= 1e-10
+
+
+def _hi(p):
+    """The IEEE high word of non-negative doubles, as the kernel compares powers (orders like the value)."""
+    return (np.ascontiguousarray(p, dtype=np.float64).view(np.uint64) >> np.uint64(32)).astype(np.int64)
+
+
+@pytest.mark.parametrize("n,wb,k,pmin,pmax", [(2048, 16, 8, 18.0, 200.0), (1024, 32, 8, 5.0, 200.0),
+                                             (4096, 16, 3, 18.0, 200.0), (2048, 16, 8, 2.0, 10.0)])
+def test_probe_threshold_candidates_superset(n, wb, k, pmin, pmax):
+    """The probe-threshold scan of the hop = 1 top-k kernel (sliding_core.h slide_topk_p_kernel) restated on
+    the oracle's band powers: in window w the probes are the k bins that won window w - WB, tau is their
+    smallest power in window w (k distinct bins of this window, so tau <= its k-th largest power), and the
+    candidates are the bins whose high word is >= hi(tau) - 1.  Every member of the window's top k -- ties at
+    the k-th included -- must be a candidate, and the reference's insertion over the candidates alone
+    (ascending bins, strict '>') must give the full scan's records.  Also reports how many candidates a window
+    has (the kernel's list holds 16; a window with more takes the exact scan)."""
+    nwin = 1500
+    s = synth.random_walk(nwin + n - 1, seed=n + wb)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = int(np.ceil(n / pmax)), min(int(np.floor(n / pmin)), n // 2 - 1)
+    band = spec[:, kmin:kmax + 1]
+    counts = []
+    for w in range(wb, nwin):
+        prev = band[w - wb]
+        probes = np.lexsort((np.arange(prev.size), -prev))[:k]  # winners of the slot's previous window
+        tau_hi = _hi(band[w, probes]).min()
+        cand = np.nonzero(_hi(band[w]) >= tau_hi - 1)[0]
+        counts.append(cand.size)
+        order = np.lexsort((np.arange(band[w].size), -band[w]))
+        kth = band[w, order[k - 1]]
+        assert set(np.nonzero(band[w] >= kth)[0]) <= set(cand), w  # ties at the k-th included
+        # the insertion over the candidates only (ascending bins, strict '>') = the full scan's top k
+        top = []
+        for j in cand:
+            p = band[w, j]
+            pos = next((i for i, (tp, _) in enumerate(top) if p > tp), len(top))
+            top.insert(pos, (p, j))
+            del top[k:]
+        assert [j for _, j in top] == list(order[:k]), w
+    counts = np.array(counts)
+    assert np.median(counts) <= 16  # the list's capacity holds the typical window (the rest: exact scan)
