@@ -75,6 +75,13 @@ def parse(argv=None):
                          "symbol spread over --c5-streams streams (round-2 form, ablation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
+    ap.add_argument("--c5-shard", default="split", choices=["split", "split-time", "symbols"],
+                    help="C5 under --scaling strong: cut the symbols' windows on one cost line into equal parts "
+                         "(McNaughton wrap-around; cost per window = output bytes, or split-time: the measured "
+                         "time per window of each length) or assign whole symbols greedily by output bytes")
+    ap.add_argument("--emulate-shard", default="",
+                    help="R/G: run exactly rank R's part of the --scaling strong split over G ranks on this one GPU "
+                         "(single-GPU emulation of one rank of a G-GPU run, not a scaling measurement)")
     ap.add_argument("--plan-only", action="store_true",
                     help="print every rank's shard of the batch and exit, without touching a GPU (CPU tests)")
     return ap.parse_args(argv)
@@ -257,6 +264,24 @@ def load_traffic(config: str):
         return None
 
 
+def load_valu(config: str):
+    """VALU-issue roofline of a VALU-bound configuration (profiles/valu.json, scripts/valu_roofline.py), or None."""
+    p = ROOT / "profiles" / "valu.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text()).get(config)
+    except Exception:
+        return None
+    if not d:
+        return None
+    return {"kernel": d["kernel"], "issue_frac": d["issue_frac"], "clock_ghz": d["clock_ghz"],
+            "valu_insts_per_wave": d.get("valu_insts_per_wave"), "wave_active_frac": d.get("wave_active_frac"),
+            "source": d["source"],
+            "definition": "4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x SQ_BUSY_CYCLES / 32): share of the SIMDs' "
+                          "4-cycle wave64 VALU issue slots in use (scripts/valu_roofline.py)"}
+
+
 class Workload:
     """What one rank runs: step() enqueues one step on `stream`; `windows` / `alg_bytes` are this
     rank's per step."""
@@ -266,6 +291,7 @@ class Workload:
     describe = ""
     cpu_cfg = None      # (series tensor, cfg) for the CPU baseline
     traffic = None      # PMC HBM bytes per step, from profiles/traffic.json
+    valu = None         # VALU-issue roofline (VALU-bound configurations), from profiles/valu.json
 
     def step(self):
         raise NotImplementedError
@@ -274,17 +300,36 @@ class Workload:
         pass
 
 
-def shard_plan(name: str, rank: int, world: int, scaling: str) -> dict:
+C5_BARS, C5_LENS = 20000, (512, 1024, 2048, 4096)
+# C5 cost per window of each length for --c5-shard split-time: the round-3 kernel trace of the grouped plan
+# (profiles/r03/c5_kernel_stats.csv: 374 / 235 / 122 / 69 us for the 4096 / 2048 / 1024 / 512 launches over
+# 7 symbols each), in units of 10 ps per window; output bytes alone (N / 2) undercount the short windows
+C5_TIME_WEIGHTS = {512: 51, 1024: 92, 2048: 187, 4096: 336}
+
+
+def c5_symbols():
+    """(window length, window count) of C5's 28 symbols: 7 per length, 20000 bars each."""
+    return [(C5_LENS[s // 7], C5_BARS - C5_LENS[s // 7] + 1) for s in range(28)]
+
+
+def shard_plan(name: str, rank: int, world: int, scaling: str, c5_shard: str = "split") -> dict:
     """This rank's part of a configuration: windows [w0, w0+nw) and series samples [a, b) (the
     N - hop halo included) of one batch (strong), or a whole batch of its own (weak); for C5 the
-    symbols it owns."""
+    pieces (symbol, first window, windows) it owns."""
     from wavespec_amd import sharding, synth
     if name == "c5":
-        bars, lens = 20000, (512, 1024, 2048, 4096)
-        nwins = [bars - lens[s // 7] + 1 for s in range(28)]
-        owned = (sharding.shard_symbols([nw * lens[s // 7] // 2 for s, nw in enumerate(nwins)], world, rank)
-                 if scaling == "strong" else list(range(28)))
-        return {"rank": rank, "symbols": owned, "windows": sum(nwins[s] for s in owned),
+        syms = c5_symbols()
+        nwins = [nw for _, nw in syms]
+        if scaling != "strong":
+            pieces = [(s, 0, nw) for s, nw in enumerate(nwins)]
+        elif c5_shard == "symbols":
+            owned = sharding.shard_symbols([nw * n // 2 for n, nw in syms], world, rank)
+            pieces = [(s, 0, nwins[s]) for s in owned]
+        else:
+            cost = [n // 2 if c5_shard == "split" else C5_TIME_WEIGHTS[n] for n, _ in syms]
+            pieces = [tuple(p) for p in sharding.split_symbols(cost, nwins, world, rank)]
+        return {"rank": rank, "symbols": sorted({p[0] for p in pieces}), "pieces": [list(p) for p in pieces],
+                "windows": sum(p[2] for p in pieces), "split": c5_shard if scaling == "strong" else None,
                 "seed_offset": 0 if scaling == "strong" else 1000 * rank}
     cfg = synth.CONFIGS[name]
     w, n, hop = cfg["windows"], cfg["n"], cfg["hop"]
@@ -345,7 +390,8 @@ class SingleBatch(Workload):
         self.f32 = f32
         self.cfg = cfg
         self.cpu_cfg = (self.series, cfg)
-        self.traffic = load_traffic(name if algo == "auto" else f"{name}_{algo}")
+        self.traffic = load_traffic(name if algo == "auto" else f"{name}_{algo}") if scaling != "strong" else None
+        self.valu = load_valu(name) if (algo, variant) == ("auto", 0) else None
         shard = f", windows [{w0}, {w0 + nw}) of {w}" if scaling == "strong" else ""
         self.describe = (f"{name}: {w} windows x {n}-pt, hop={hop}, {cfg['precision']}, {cfg['detrend']} detrend, "
                          f"{cfg['window']} window, " + {
@@ -365,30 +411,40 @@ class SingleBatch(Workload):
 class C5Batch(Workload):
     """C5: 28 symbols x 20000 bars, N in {512,1024,2048,4096} (7 symbols each), hop = 1, fp64,
     Hann -- the WaveCyclesBatchFetcher shape (WaveCyclesBatchFetcher.mq5:106-133: one batch per
-    symbol).  One step = every owned symbol's batch.  Default (--c5-mode group): one grouped device
-    plan (wsp_group_*), the symbols of each window length in one sliding-DFT launch on the launch
-    stream.  --c5-mode plans: one plan per symbol, spread over --c5-streams streams joined into the
+    symbol).  One step = every owned piece's batch (a whole symbol, or under --scaling strong a
+    window range of one with its N - 1 halo).  Default (--c5-mode group): one grouped device plan
+    (wsp_group_*), the pieces of each window length in one sliding-DFT launch on the launch
+    stream.  --c5-mode plans: one plan per piece, spread over --c5-streams streams joined into the
     launch stream (the round-2 form)."""
 
     def __init__(self, rank, local_rank, world, scaling, algo="auto", slide_seg=0, c5_layout="greedy", c5_streams=3,
-                 c5_mode="group"):
+                 c5_mode="group", c5_shard="split"):
         import torch
         from wavespec_amd import bridge, synth
         dev = torch.device("cuda", local_rank)
-        bars, lens = 20000, (512, 1024, 2048, 4096)
-        nwins = [bars - lens[s // 7] + 1 for s in range(28)]
-        sp = shard_plan("c5", rank, world, scaling)
-        owned, seed_off = sp["symbols"], sp["seed_offset"]
+        syms = c5_symbols()
+        sp = shard_plan("c5", rank, world, scaling, c5_shard)
+        pieces, seed_off = [tuple(p) for p in sp["pieces"]], sp["seed_offset"]
         self.f32 = False
         self.stream = torch.cuda.current_stream(dev)
         self.group = None
-        self.describe = (f"c5: 28 symbols x {bars} bars, N in {lens} (7 each), hop=1, f64, Hann, |X|^2"
-                         + (f", {len(owned)} symbols on this rank" if scaling == "strong" else ""))
+        self.describe = (f"c5: 28 symbols x {C5_BARS} bars, N in {C5_LENS} (7 each), hop=1, f64, Hann, |X|^2"
+                         + (f", rank {rank}/{world} of a {c5_shard} split: {len(pieces)} pieces of "
+                            f"{len(sp['symbols'])} symbols" if scaling == "strong" else ""))
+        full = {}
+
+        def piece_series(sym, w0, nw):  # the symbol's bars, then the piece's windows + N - 1 halo (resident in HBM)
+            if sym not in full:
+                full[sym] = synth.random_walk_torch(C5_BARS, 100 + sym + seed_off, dev)
+            x = full[sym]
+            n = syms[sym][0]
+            return x if (w0, nw) == (0, syms[sym][1]) else x[w0: w0 + nw - 1 + n].contiguous()
+
+        lens = [syms[p[0]][0] for p in pieces]
         if c5_mode == "group" and algo in ("auto", "slide"):
-            self.series = [synth.random_walk_torch(bars, 100 + sym + seed_off, dev) for sym in owned]
-            self.outs = [torch.empty(nwins[sym] * (lens[sym // 7] // 2), dtype=torch.float64, device=dev)
-                         for sym in owned]
-            self.group = bridge.Group(local_rank, [lens[sym // 7] for sym in owned], [nwins[sym] for sym in owned])
+            self.series = [piece_series(*p) for p in pieces]
+            self.outs = [torch.empty(p[2] * (n // 2), dtype=torch.float64, device=dev) for p, n in zip(pieces, lens)]
+            self.group = bridge.Group(local_rank, lens, [p[2] for p in pieces])
             if c5_streams:
                 self.group.set_streams(c5_streams)
             if slide_seg:
@@ -396,58 +452,61 @@ class C5Batch(Workload):
             self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
             self.algorithm = "slide-group"
             self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams or "library default",
-                           "segment": slide_seg or "auto"}
-            self.windows = sum(nwins[sym] for sym in owned)
+                           "segment": slide_seg or "auto", "pieces": len(pieces)}
+            self.windows = sum(p[2] for p in pieces)
             self.alg_bytes = self.group.algorithmic_bytes
-            self.traffic = load_traffic("c5")
-            i4 = [i for i, sym in enumerate(owned) if lens[sym // 7] == 4096]
-            if i4:
-                self.cpu_cfg = (self.series[i4[-1]], {"n": 4096, "hop": 1, "windows": nwins[owned[i4[-1]]],
-                                                      "detrend": "none", "window": "hann"})
+            self.traffic = load_traffic("c5") if scaling != "strong" else None
+            i4 = [i for i, n in enumerate(lens) if n == 4096]
+            i = i4[-1] if i4 else len(pieces) - 1
+            self.cpu_cfg = (self.series[i], {"n": lens[i], "hop": 1, "windows": pieces[i][2], "detrend": "none",
+                                             "window": "hann"})
+            full.clear()
             return
         # Three streams, within the box's 4 HIP hardware queues together with the launch stream (with
         # one stream per length two of them shared a hardware queue and ran 14 kernels back to back:
         # the whole step, profiles/r02/c5_kernel_stats.csv).  --c5-layout: "length" puts {4096}, {2048},
-        # {1024, 512} on their own streams; "greedy" assigns symbols longest-first to the least-loaded
+        # {1024, 512} on their own streams; "greedy" assigns pieces longest-first to the least-loaded
         # stream by output bytes (what the hop = 1 sliding DFT's time follows: nwin x N/2), "nlogn" the
-        # same by windows x N log N (the FFT kernel's work).  --c5-streams 1 runs every symbol on one
+        # same by windows x N log N (the FFT kernel's work).  --c5-streams 1 runs every piece on one
         # stream (ablation).
         nstreams = c5_streams or 3
         self.streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
         if c5_layout == "nlogn":
-            cost = {sym: nwins[sym] * lens[sym // 7] * int(np.log2(lens[sym // 7])) for sym in owned}
+            cost = [p[2] * n * int(np.log2(n)) for p, n in zip(pieces, lens)]
         else:
-            cost = {sym: nwins[sym] * (lens[sym // 7] // 2) for sym in owned}
+            cost = [p[2] * (n // 2) for p, n in zip(pieces, lens)]
+        order = sorted(range(len(pieces)), key=lambda i: -cost[i])
         load, assign = [0] * nstreams, {}
         if c5_layout in ("greedy", "nlogn"):
-            for sym in sorted(owned, key=lambda x: -cost[x]):
+            for i in order:
                 k = load.index(min(load))
-                assign[sym] = k
-                load[k] += cost[sym]
+                assign[i] = k
+                load[k] += cost[i]
         else:  # by window length: {4096}, {2048}, {1024, 512}
-            for sym in owned:
-                assign[sym] = {4096: 0, 2048: 1, 1024: 2, 512: 2}[lens[sym // 7]] % nstreams
+            for i in order:
+                assign[i] = {4096: 0, 2048: 1, 1024: 2, 512: 2}[lens[i]] % nstreams
         self.layout = {"layout": c5_layout, "streams": nstreams,
-                       "stream_load": [sum(cost[x] for x in owned if assign[x] == k) for k in range(nstreams)]}
+                       "stream_load": [sum(cost[i] for i in order if assign[i] == k) for k in range(nstreams)]}
         self.jobs = []  # (plan, series, out, stream), launched longest first
-        for sym in sorted(owned, key=lambda x: -cost[x]):
-            n = lens[sym // 7]
-            series = synth.random_walk_torch(bars, 100 + sym + seed_off, dev)
-            out = torch.empty(nwins[sym] * (n // 2), dtype=torch.float64, device=dev)
-            plan = bridge.Plan(local_rank, n, 1, nwins[sym], "none", "hann")
+        for i in order:
+            n, nw = lens[i], pieces[i][2]
+            series = piece_series(*pieces[i])
+            out = torch.empty(nw * (n // 2), dtype=torch.float64, device=dev)
+            plan = bridge.Plan(local_rank, n, 1, nw, "none", "hann")
             if algo != "auto":
                 plan.set_algorithm(algo)
             if slide_seg:
                 plan.set_slide_segment(slide_seg)
-            self.jobs.append((plan, series, out, self.streams[assign[sym]]))
+            self.jobs.append((plan, series, out, self.streams[assign[i]]))
+        full.clear()
         self.algorithm = "+".join(sorted({j[0].algorithm() for j in self.jobs}))
         self.windows = sum(j[0].n_windows for j in self.jobs)
         self.alg_bytes = sum(j[0].algorithmic_bytes for j in self.jobs)
-        self.traffic = load_traffic("c5_plans" if algo == "auto" else f"c5_{algo}")  # PMC bytes per step (28 plans)
-        big = [j for j in self.jobs if j[0].window_len == 4096]
-        if big:  # a 4096-pt symbol: the costliest per window
-            p0, s0 = big[-1][0], big[-1][1]
-            self.cpu_cfg = (s0, {"n": 4096, "hop": 1, "windows": p0.n_windows, "detrend": "none", "window": "hann"})
+        self.traffic = load_traffic("c5_plans" if algo == "auto" else f"c5_{algo}") if scaling != "strong" else None
+        big = [j for j in self.jobs if j[0].window_len == 4096] or self.jobs
+        p0, s0 = big[-1][0], big[-1][1]
+        self.cpu_cfg = (s0, {"n": p0.window_len, "hop": 1, "windows": p0.n_windows, "detrend": "none",
+                             "window": "hann"})
 
     def step(self):
         if self.group is not None:
@@ -476,15 +535,24 @@ def main(argv=None):
         return launch_ranks(args, argv)
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+    shard_rank, shard_world, scaling = rank, world, args.scaling
+    if args.emulate_shard:
+        try:
+            shard_rank, shard_world = (int(v) for v in args.emulate_shard.split("/"))
+        except ValueError:
+            raise SystemExit("--emulate-shard takes R/G, e.g. 3/8")
+        if world != 1 or not 0 <= shard_rank < shard_world:
+            raise SystemExit("--emulate-shard R/G runs one rank's shard on one GPU: 0 <= R < G, --gpus 1")
+        scaling = "strong"
     if args.plan_only:
         ctl = Control(world)
-        mine = shard_plan(args.config, rank, world, args.scaling)
+        mine = shard_plan(args.config, shard_rank, shard_world, scaling, args.c5_shard)
         parts = [mine]
         if world > 1:
             parts = [None] * world
             ctl.dist.all_gather_object(parts, mine)
         if rank == 0:
-            print(json.dumps({"n_gpus": world, "config": args.config, "scaling": args.scaling, "shards": parts}),
+            print(json.dumps({"n_gpus": world, "config": args.config, "scaling": scaling, "shards": parts}),
                   flush=True)
         ctl.close()
         return 0
@@ -494,10 +562,11 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     ctl = Control(world)
     if args.config == "c5":
-        wl = C5Batch(rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.c5_layout, args.c5_streams,
-                     args.c5_mode)
+        wl = C5Batch(shard_rank, local_rank, shard_world, scaling, args.algo, args.slide_seg, args.c5_layout,
+                     args.c5_streams, args.c5_mode, args.c5_shard)
     else:
-        wl = SingleBatch(args.config, rank, local_rank, world, args.scaling, args.algo, args.slide_seg, args.variant)
+        wl = SingleBatch(args.config, shard_rank, local_rank, shard_world, scaling, args.algo, args.slide_seg,
+                         args.variant)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)
@@ -528,19 +597,26 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": secs / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32" if wl.f32 else "f64",
             "data": "synthetic (random-walk close prices generated on device, seed per rank)",
             "config": {"workload": wl.describe, "windows_per_gpu": wl.windows, "windows_total": int(total_windows / args.steps),
                        "parallelism": f"windows sharded x{world} ({args.scaling}), no collective",
                        "algorithm": wl.algorithm, **({"c5": wl.layout} if hasattr(wl, "layout") else {})},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "valu" if wl.valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
+                         "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a "
+                                           "separate run, scripts/parse_prof.py), not this run" if wl.traffic else None,
+                         **({"valu": wl.valu, "note": "VALU-issue-bound: achieved / frac are the HBM roofline, "
+                                                      "valu.issue_frac the bound's"} if wl.valu else {}),
                          "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,
                          "kernel_ms_max_over_ranks": kernel_s_max * 1e3,
                          "timing": "HIP events on the launch stream around the same K timed steps (rank 0)"},
             "settle": settled,
+            **({"emulated_shard": {"rank": shard_rank, "of": shard_world, "split": args.c5_shard if args.config == "c5" else "windows",
+                                   "caveat": "single-GPU emulation of one rank of a strong-scaled run, not a scaling "
+                                             "measurement"}} if args.emulate_shard else {}),
             "cpu_baseline": baseline,
             "cpu_baseline_all_cores": baseline_all,
         }

@@ -309,6 +309,7 @@ struct Config {
     int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
     int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
     int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
+    unsigned char *scan_flags = nullptr;  // wsp_plan_set_scan_flags: per-window path of the probe-threshold top-k scan
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
     int64_t record() const {
@@ -342,24 +343,30 @@ bool use_slide_topk(const Config &c);
 // SIMD = 16 per CU) at <= 256 windows each -- C4 (1,048,576 windows): one round of 4096 segments of 256,
 // 0.371-0.374 ms against 0.389 for 128-window segments (two rounds) and 0.41 / 0.50 for 192 / 384
 // (1.33 rounds / a quarter of the slots idle; profiles/r03/s2/topk_seg.log).  At least 64 windows.
-int64_t slide_topk_seg(const Config &c) {
+// CUs of device `dev`, looked up once per device (the segment policy of a plan follows its own GPU, not the
+// calling thread's current one)
+int cu_count(int dev) {
+    static std::atomic<int> cache[64];
+    if (dev < 0 || dev >= 64) return 256;
+    int cus = cache[dev].load(std::memory_order_relaxed);
+    if (cus > 0) return cus;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
+int64_t slide_topk_seg(const Config &c, int dev) {
     if (c.slide_seg > 0) return c.slide_seg;
-    static const int64_t res = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus <= 0)
-            cus = 256;
-        return (int64_t)16 * cus;
-    }();
+    const int64_t res = (int64_t)16 * cu_count(dev);
     const int64_t rounds = (c.n_windows + res * 256 - 1) / (res * 256);
     const int64_t seg = (c.n_windows + res * rounds - 1) / (res * rounds);
     return seg < 64 ? 64 : seg;
 }
-WsLayout ws_layout(const Config &c) {
+WsLayout ws_layout(const Config &c, int dev) {
     WsLayout L;
     if (use_slide_topk(c)) {
         const int nf = window_coef(c.window).nf;
-        const int64_t nseg = (c.n_windows + slide_topk_seg(c) - 1) / slide_topk_seg(c);
+        const int64_t seg = slide_topk_seg(c, dev);
+        const int64_t nseg = (c.n_windows + seg - 1) / seg;
         L.total = (size_t)nseg * (size_t)slide_topk_seed_stride(nf, c.kmax - c.kmin + 1) * 2 * sizeof(double);
         return L;
     }
@@ -517,7 +524,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         HIP_OR(launch_inverse(I, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
-    const WsLayout ws = ws_layout(c);
+    const WsLayout ws = ws_layout(c, dev);
     char *wsb = static_cast<char *>(d_ws);
     if (c.log2n > kMaxLog2N) {  // N > 16384: four-step transform (large_fft.hip)
         LargeLaunch G{};
@@ -565,12 +572,13 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         A.out = d_out;
         A.n_windows = c.n_windows;
         if (topk) {
-            A.seg = slide_topk_seg(c);
+            A.seg = slide_topk_seg(c, dev);
             A.variant = c.variant;
             A.kmin = c.kmin;
             A.span = c.kmax - c.kmin + 1;
             A.topk = c.topk;
             A.ws = d_ws;
+            A.flags = c.scan_flags;
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }
@@ -834,7 +842,7 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             pc.n_windows = p.nw;
             p.in_bytes = (size_t)pc.series_elems() * es;
             p.out_bytes = (size_t)(p.nw * c.record()) * es;
-            p.ws_bytes = ws_layout(pc).total;
+            p.ws_bytes = ws_layout(pc, D.dev).total;
             p.stream = D.next_stream();
             b->parts.push_back(p);
             Part &P = b->parts.back();
@@ -1018,15 +1026,16 @@ std::shared_ptr<void> plan_ws_alloc(int dev, size_t bytes) {
 // (under p->mu) grow the workspace to what cfg needs
 int plan_ws_fit(Plan &p) {
     ws_reap();
-    const size_t need = ws_layout(p.cfg).total;
+    const size_t need = ws_layout(p.cfg, p.dev).total;
     if (need <= p.ws_bytes) return MTB_OK;
     auto w = plan_ws_alloc(p.dev, need);
     if (!w) {
         set_error("hipMalloc(%zu) for the plan workspace failed", need);
         return MTB_NO_MEM;
     }
-    p.ws = std::move(w);
+    p.ws = std::move(w);  // the old block is parked now, unless an execute still holds it
     p.ws_bytes = need;
+    ws_reap();            // ... and freed here rather than at the next configuration call
     return MTB_OK;
 }
 std::mutex g_plans_mu;
@@ -1742,6 +1751,17 @@ MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     }
     std::lock_guard<std::mutex> lk(p->mu);
     p->cfg.variant = variant;
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_plan_set_scan_flags(int64_t plan, void *d_flags) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p) {
+        set_error("wsp_plan_set_scan_flags(%lld): unknown plan", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.scan_flags = static_cast<unsigned char *>(d_flags);
     return MTB_OK;
 }
 

@@ -780,12 +780,14 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
                     base += __popcll(bal[b]);
                 }
                 if (l == 0) cnt[slot] = total;
+                if (a.flags && l == 0) a.flags[w0 + wi] = 0;
             } else {  // exact one-wave scan of this window; its winners probe the slot from now on
 #pragma unroll
                 for (int b = 0; b < NB; ++b) xb[l + 64 * b] = core::cpx<double>{X[b].x, X[b].y};
                 __syncthreads();
                 core::topk_wave64<NB, double>(xb, kmin, span, kk, l, rec + (int64_t)wi * (4 * kk), true, win);
                 if (l == 0) cnt[slot] = -1;
+                if (a.flags && l == 0) a.flags[w0 + wi] = wi == 0 ? 1 : 2;
                 __syncthreads();
                 if (l < kk && win[l] >= 0) atomicOr(&nm[win[l]], 1u << slot);
                 __syncthreads();

@@ -81,7 +81,9 @@ struct LargeLaunch {
     int packed;           // 0 power, 1 packed (Re, Im)
     bool f32;
     double iir_alpha, iir_c;
-    int variant;          // ablations: 0 default (two-pass), 2 pipelined quarter chunks on two streams, 3 fused (512 threads, no prefetch), 4 fused (256 threads, prefetch)
+    int variant;          // wsp_plan_set_variant (include/mtbridge.h): 0 = the library's choice (fused non-temporal kernel for
+                          // fp64 N = 65536, two passes otherwise), 1 two passes, 2 two passes pipelined over two streams,
+                          // 3 fused (512 threads), 4 fused (256 threads, register prefetch), 5 fused with plain stores
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
@@ -123,7 +125,10 @@ struct SlideArgs {
     // top-k records (launch_slide_topk, fp64): bins [kmin, kmin + span), topk slots, seeds workspace
     int kmin, span, topk;
     void *ws;             // ceil(n_windows / seg) * slide_topk_seed_stride(nf, span) double complex
-    int variant;          // top-k scan: 0 = auto, 1 = one wave per window, 2 / 3 = transposed, 16 / 8 windows per batch
+    int variant;          // top-k scan (wsp_plan_set_variant): 0 = probe threshold (16 windows x 16 candidates, 4 waves
+                          // per SIMD), 1 = one wave per window, 2 / 3 = transposed, 16 / 8 windows per batch,
+                          // 4 / 5 = probe threshold at 32 windows x 16 / 12 candidates
+    unsigned char *flags; // probe-threshold top-k scan: per-window path (wsp_plan_set_scan_flags), nullptr = off
     double share;         // launches running side by side (grouped plan on several streams): the launcher's
                           // segments fill 1/share of the resident workgroup slots; 0 / 1 = all of them
 };

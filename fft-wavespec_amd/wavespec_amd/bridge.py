@@ -68,6 +68,7 @@ SIGNATURES = {
     "wsp_plan_get_algorithm": (C.c_int32, [C.c_int64]),
     "wsp_plan_set_slide_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_plan_set_variant": (C.c_int32, [C.c_int64, C.c_int32]),
+    "wsp_plan_set_scan_flags": (C.c_int32, [C.c_int64, C.c_void_p]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -320,6 +321,11 @@ class Plan:
     def set_variant(self, variant: int) -> None:
         """Ablation: the kernel form (include/mtbridge.h wsp_plan_set_variant; 0 = the library's choice)."""
         _check("wsp_plan_set_variant", lib().wsp_plan_set_variant(self.handle, variant))
+
+    def set_scan_flags(self, d_flags: int) -> None:
+        """Diagnostics: device buffer of n_windows bytes receiving each window's top-k scan path
+        (0 candidate list, 1 segment start, 2 candidate overflow), or 0 = off."""
+        _check("wsp_plan_set_scan_flags", lib().wsp_plan_set_scan_flags(self.handle, C.c_void_p(d_flags)))
 
     def algorithm(self) -> str:
         """What the next execute runs: "fft" or "slide"."""

@@ -313,6 +313,13 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter. */
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);
+/* Diagnostics: d_flags (device, n_windows bytes, or NULL = off) receives, on
+ * every execute of a hop = 1 top-k plan by the probe-threshold scan (variant
+ * 0 / 4 / 5), the path each window took: 0 = the candidate list, 1 = the exact
+ * one-wave scan at a segment's first window, 2 = the exact scan because more
+ * candidates passed the threshold than the list holds.  Other plans leave it
+ * untouched.  The records are the same either way. */
+MTB_API int32_t wsp_plan_set_scan_flags(int64_t plan, void *d_flags);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
 
@@ -332,9 +339,14 @@ MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan);
  * a handle > 0, or 0 (see gpu_get_last_error_w). */
 MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_t *window_len,
                                  const int64_t *n_windows, int32_t detrend, int32_t window, int32_t precision);
-/* Enqueues every member on `hip_stream`: d_series[m] / d_out[m] are device
- * pointers (double or float per the precision).  Asynchronous, no host sync;
- * a group has no workspace, so executes may run concurrently. */
+/* Enqueues every member: d_series[m] / d_out[m] are device pointers (double
+ * or float per the precision).  Asynchronous, no host sync.  The launches
+ * start on `hip_stream` and, with more than one lane (wsp_group_set_streams),
+ * fork onto the group's internal streams and join back into `hip_stream`
+ * (events): work enqueued on `hip_stream` after the execute sees every
+ * member's output.  The internal streams belong to the group and every execute
+ * uses them, so executes of one group issued on different caller streams run
+ * one after another, not concurrently (use one group per concurrent caller). */
 MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, void *const *d_out, void *hip_stream);
 /* Algorithmic bytes of one execute (sum over members, as wsp_plan_algorithmic_bytes). */
 MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
@@ -345,7 +357,9 @@ MTB_API int32_t wsp_group_launches(int64_t group);
  * joined back (events; no host sync) -- assigned greedily by output bytes,
  * each lane's launches sized for its share of the device's workgroup slots,
  * so one window length's seed phase and last workgroups overlap the others'.
- * 1 (default) = everything on the caller's stream.  MTB_BAD_ARGS outside 1..8. */
+ * Default (set by wsp_group_create): one lane per launch, at most 4 (the HIP
+ * hardware queues of a process); 1 = everything on the caller's stream.
+ * MTB_BAD_ARGS outside 1..8. */
 MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams);
 /* Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy over
  * each window length's total window count), at most 2048. */

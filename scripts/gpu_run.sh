@@ -18,6 +18,8 @@
 #   kbench=<args>            fft-wavespec_amd/bin/kbench <args> (spaces as commas)
 #   kalman=<args>            fft-wavespec_amd/bin/kalman_bench <args>
 #   harness=<args>           python scripts/<args> (a host-path timing script), spaces as commas
+#   shards[=<args>]          python scripts/emulate_shards.py <tag dir>/shards.json <args> (strong-scaling shards
+#                            emulated one rank at a time on this GPU), args comma-separated
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -93,6 +95,10 @@ print('$cfg', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g wi
         hl=$O/harness_${val//,/_}.log
         run 300 $hl $hl python3 scripts/${val//,/ }
         cat $hl
+        ;;
+    shards)
+        run 1100 $O/shards.log $O/shards.log python3 -u scripts/emulate_shards.py $O/shards.json ${val//,/ }
+        cat $O/shards.log
         ;;
     *)
         echo "unknown step $step"

@@ -205,6 +205,64 @@ def test_ns_topk_full_grid(gpu_session, output):
     plan.close()
 
 
+def test_c4_topk_probe_scan_vs_oracle_full_size(gpu_session):
+    """The benchmarked hop = 1 top-8 scan (c4_topk: 1,048,576 windows x 2048, the default probe-threshold kernel,
+    L/WaveSpecZZ_1.0.3-pla-kalman-fast-gpuopt-nodetrend.mq5:536-554) against the oracle's ora_batch_topk at full
+    size, on windows sampled where the scan's paths meet: both ends of the batch, the segment seams (every
+    segment start the policy chose, with the window before it and the first window of the next staged batch),
+    every window where more candidates passed the threshold than the list holds (the exact-scan fallback,
+    flagged by the kernel through wsp_plan_set_scan_flags), and a random spread.  Records the fallback rate."""
+    torch = pytest.importorskip("torch")
+    n, nwin, k = 2048, 1_048_576, 8
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(nwin + n - 1, 13, dev)
+    plan = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+    plan.set_topk(k, 18.0, 200.0)
+    assert plan.algorithm() == "slide"
+    d_o = torch.empty(nwin * 4 * k, dtype=torch.float64, device=dev)
+    flags = torch.full((nwin,), 255, dtype=torch.uint8, device=dev)
+    plan.set_scan_flags(flags.data_ptr())
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    # the records without the diagnostics are the same
+    d_o2 = torch.empty_like(d_o)
+    plan.set_scan_flags(0)
+    plan.execute(d_s.data_ptr(), d_o2.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(d_o, d_o2)
+    del d_o2
+    f = flags.cpu().numpy()
+    assert f.max() <= 2, "every window reports its path"
+    starts = np.flatnonzero(f == 1)
+    over = np.flatnonzero(f == 2)
+    seg = np.diff(starts)
+    assert starts[0] == 0 and len(starts) >= 1
+    rng = np.random.default_rng(4)
+    seams = starts[1:] if len(starts) <= 600 else rng.choice(starts[1:], 600, replace=False)
+    over_s = over if len(over) <= 3000 else rng.choice(over, 3000, replace=False)
+    idx = np.unique(np.r_[np.arange(64), np.arange(nwin - 64, nwin), seams - 1, seams, seams + 16, over_s,
+                          rng.integers(0, nwin, 2000)])
+    idx = idx[(idx >= 0) & (idx < nwin)]
+    host = d_s.cpu().numpy()
+    R = d_o.view(nwin, k, 4)
+    got = R[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.concatenate([oracle.batch_topk(host[i:i + n], n, 1, "none", "hann", 0, None, k, 18.0, 200.0)
+                           for i in idx])
+    kmin, kmax = oracle.band(n)
+    band_max = np.array([oracle.window_spectrum(host[i:i + n], "none", "hann")[kmin:kmax + 1].max() for i in idx])
+    same = got[:, :, 0] == want[:, :, 0]
+    _record("c4_topk_full_size", windows_checked=int(len(idx)), segments=int(len(starts)),
+            segment_lengths=sorted({int(x) for x in seg}) + [int(nwin - starts[-1])],
+            fallback_windows=int(len(over)), fallback_rate=float(len(over) / nwin),
+            checked_fallbacks=int(len(over_s)), bin_mismatches=int((~same).sum()))
+    print(f"c4_topk: {len(starts)} segments, {len(over)} overflow fallbacks ({len(over) / nwin:.2e} of windows), "
+          f"{len(idx)} windows checked, {int((~same).sum())} rank swaps")
+    from test_gpu_slide import _topk_bars
+    _topk_bars(got, want, band_max, max_swaps=8)
+    del d_o
+    plan.close()
+
+
 # ------------------------------------------------------------------ C5 concurrency
 def _fetcher(sym, n, series, res, barrier_a, barrier_b, early):
     """WaveCyclesBatchFetcher::OnTimer (WaveCyclesBatchFetcher.mq5:104-133) on the spectrum batch API:

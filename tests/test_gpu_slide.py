@@ -267,6 +267,48 @@ def test_slide_topk_scan_forms_identical(gpu_session, n, pmin, pmax, seg):
     _topk_bars(outs[0], want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
 
 
+@pytest.mark.parametrize("case", ["zeros", "ones_mean", "zeros_then_walk"])
+def test_slide_topk_exact_ties(gpu_session, case):
+    """Exactly tied band powers: a zero series (every tracker stays exactly 0), a constant 1.0 with
+    the mean detrend (x - mean = 0 exactly), and zeros, then a random walk (windows leaving the all-tie state
+    mid-segment: the probe bins of an all-tie batch meet real powers).  With every power equal the reference's strict '>' insertion keeps the first k
+    bins of the band in ascending order (gpuopt-nodetrend.mq5:545-552); the probe-threshold forms (variants 0,
+    4, 5: the hi-word threshold with one step of slack and the 4-lane bitonic merge) must give records
+    identical to the one-wave scan (variant 1) and to the transposed scan (2, 3), and the oracle's bars."""
+    torch = pytest.importorskip("torch")
+    n, nwin, k = 2048, 1500, 8
+    rng_walk = synth.random_walk(nwin + n - 1, seed=91)
+    detrend = "mean" if case == "ones_mean" else "none"
+    if case == "zeros":
+        s = np.zeros(nwin + n - 1)
+    elif case == "ones_mean":
+        s = np.ones(nwin + n - 1)
+    else:
+        s = np.zeros(nwin + n - 1)
+        s[2600:] = rng_walk[2600:] - 1.1  # windows 0 .. 552 are all zeros, 553 .. 1499 see the walk
+    outs = []
+    for v in range(6):
+        plan = bridge.Plan(0, n, 1, nwin, detrend, "hann", output="topk")
+        plan.set_topk(k, 18.0, 200.0)
+        plan.set_algorithm("slide")
+        plan.set_variant(v)
+        plan.set_slide_segment(100)  # seams every 100 windows: all-tie windows at segment starts and mid-batch
+        outs.append(_run(plan, s, torch).reshape(nwin, k, 4))
+        plan.close()
+    for v in range(1, 6):
+        assert np.array_equal(outs[0], outs[v]), v
+    want = oracle.batch_topk(s, n, 1, detrend, "hann", 0, None, k, 18.0, 200.0)
+    kmin, kmax = oracle.band(n)
+    tied = np.all(want[:, :, 1] == 0.0, axis=1)  # windows whose band is exactly zero
+    assert tied.sum() > 0
+    first_k = np.arange(kmin, kmin + k, dtype=np.float64)
+    assert np.all(want[tied, :, 0] == first_k)
+    assert np.all(outs[0][tied, :, 0] == first_k) and np.all(outs[0][tied, :, 1] == 0.0)
+    if (~tied).any():
+        spec = oracle.batch_spectrum(s, n, 1, detrend, "hann")
+        _topk_bars(outs[0][~tied], want[~tied], spec[~tied, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
 def test_slide_topk_vs_fft_c4(gpu_session):
     """C4's batch (1,048,576 windows x 2048) as top-8 records: sliding DFT against the FFT kernel's fused
     scan on the same device buffer, every window."""
@@ -289,6 +331,40 @@ def test_slide_topk_vs_fft_c4(gpu_session):
     assert int((~same).sum().item()) <= 64  # rank swaps between near-equal powers only
     top = B[:, 0, 1]
     assert ((A[:, :, 1] - B[:, :, 1]).abs() <= 1e-10 * top[:, None]).all().item()
+
+
+def test_plan_workspace_growth_frees_old_block(gpu_session):
+    """A reconfiguration that grows a plan's workspace frees the block it replaces at once: the
+    device's free memory drops by the growth, not by the whole new block.  Top-k seeds of 1M windows: 128-window
+    segments take ~78 MB, 64-window segments ~155 MB."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 2048, 1_000_000
+    plan = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+    plan.set_topk(8, 18.0, 200.0)
+    plan.set_algorithm("slide")
+    plan.set_slide_segment(128)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    plan.set_slide_segment(64)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info(0)[0]
+    stride = (3 * 207 + 1) * 16  # slide_topk_seed_stride(nf = 3, span = 207) double complex per segment
+    old, new = -(-nwin // 128) * stride, -(-nwin // 64) * stride
+    drop = free0 - free1
+    assert drop <= new - old + (32 << 20), (drop, old, new)
+    s = synth.random_walk(nwin + n - 1, seed=3)[: 3000 + n - 1]
+    plan.close()
+    # the plan still runs right after the growth (small batch, same configuration calls)
+    small = bridge.Plan(0, n, 1, 3000, "none", "hann", output="topk")
+    small.set_topk(8, 18.0, 200.0)
+    small.set_slide_segment(128)
+    small.set_slide_segment(64)
+    got = _run(small, s, torch).reshape(3000, 8, 4)
+    small.close()
+    want = oracle.batch_topk(s, n, 1, "none", "hann", 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = oracle.band(n)
+    _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
 
 
 def test_slide_topk_workspace_follows_reconfiguration(gpu_session):

@@ -127,7 +127,8 @@ def test_bench_gpus2_spawns_ranks_and_shards_c4():
 
 
 def test_bench_c5_strong_symbols_partition():
-    r, lines = _bench_line("--gpus", "2", "--config", "c5", "--scaling", "strong", "--plan-only")
+    r, lines = _bench_line("--gpus", "2", "--config", "c5", "--scaling", "strong", "--c5-shard", "symbols",
+                           "--plan-only")
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = lines
     syms = sorted(s for sh in line["shards"] for s in sh["symbols"])
@@ -136,6 +137,55 @@ def test_bench_c5_strong_symbols_partition():
     lens = (512, 1024, 2048, 4096)
     out_bytes = [sum((20000 - lens[s // 7] + 1) * lens[s // 7] // 2 for s in sh["symbols"]) for sh in line["shards"]]
     assert max(out_bytes) / min(out_bytes) < 1.05  # balanced by the bytes each rank writes
+
+
+@pytest.mark.parametrize("split", ["split", "split-time"])
+def test_bench_c5_strong_split_pieces(split):
+    """C5 cut on one cost line (McNaughton wrap-around, sharding.split_symbols) over a real 2-rank gloo
+    rendezvous, and over 8 ranks through --emulate-shard R/8 (one rank's plan on one process): the pieces
+    cover every window of every symbol exactly once, each rank's cost is within one window of the mean, and
+    no symbol is cut more than G - 1 times."""
+    import bench
+    lens = (512, 1024, 2048, 4096)
+    nw = [20000 - lens[s // 7] + 1 for s in range(28)]
+    cost = [(n // 2 if split == "split" else bench.C5_TIME_WEIGHTS[n]) for n in (lens[s // 7] for s in range(28))]
+    r, lines = _bench_line("--gpus", "2", "--config", "c5", "--scaling", "strong", "--c5-shard", split, "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    two = lines[0]["shards"]
+    for g, shards in ((2, two), (8, None)):
+        if shards is None:
+            shards = []
+            for rk in range(8):
+                r, ln = _bench_line("--config", "c5", "--emulate-shard", f"{rk}/8", "--c5-shard", split, "--plan-only")
+                assert r.returncode == 0, r.stderr[-2000:]
+                shards += ln[0]["shards"]
+        cover = [np.zeros(n, dtype=int) for n in nw]
+        loads = []
+        for sh in shards:
+            load = 0
+            for sym, w0, k in sh["pieces"]:
+                cover[sym][w0:w0 + k] += 1
+                load += k * cost[sym]
+            loads.append(load)
+            assert sh["windows"] == sum(p[2] for p in sh["pieces"])
+        assert all((c == 1).all() for c in cover)
+        assert max(loads) - min(loads) <= 2 * max(cost)
+        cuts = {}
+        for sh in shards:
+            for sym, _, _ in sh["pieces"]:
+                cuts[sym] = cuts.get(sym, 0) + 1
+        assert max(cuts.values()) <= g
+
+
+def test_split_symbols_unit():
+    for g in (1, 2, 3, 5, 8):
+        costs, nwins = [3, 1, 7, 2], [10, 0, 5, 9]
+        seen = [[0] * n for n in nwins]
+        for r in range(g):
+            for i, w0, k in sharding.split_symbols(costs, nwins, g, r):
+                for j in range(w0, w0 + k):
+                    seen[i][j] += 1
+        assert all(all(v == 1 for v in row) for row in seen)
 
 
 def test_bench_world_size_mismatch_fails():
@@ -166,7 +216,8 @@ def test_bench_gpus8_c4_strong_plan():
 def test_bench_gpus8_c5_and_weak_plans():
     """C5 over 8 ranks (whole symbols, balanced by output bytes within 10 %) and the weak-scaling north star
     (every rank a full 65536-window batch of its own seed)."""
-    r, lines = _bench_line("--gpus", "8", "--config", "c5", "--scaling", "strong", "--plan-only")
+    r, lines = _bench_line("--gpus", "8", "--config", "c5", "--scaling", "strong", "--c5-shard", "symbols",
+                           "--plan-only")
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = lines
     syms = sorted(s for sh in line["shards"] for s in sh["symbols"])
