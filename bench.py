@@ -70,9 +70,10 @@ def parse(argv=None):
     ap.add_argument("--c5-streams", type=int, default=0,
                     help="C5: lanes the grouped plan runs its launches on (wsp_group_set_streams; 0 = the library's "
                          "default, one per window length up to 4) / streams the symbol plans use (0 = 3)")
-    ap.add_argument("--c5-mode", default="group", choices=["group", "plans"],
-                    help="C5: one grouped device plan (wsp_group_*: one launch per window length) or one plan per "
-                         "symbol spread over --c5-streams streams (round-2 form, ablation)")
+    ap.add_argument("--c5-mode", default="group", choices=["group", "group-per-length", "plans"],
+                    help="C5: one grouped device plan (wsp_group_*: one mixed-length persistent launch), the grouped "
+                         "plan's per-length launches on lanes (round-3 form), or one plan per symbol spread over "
+                         "--c5-streams streams (round-2 form)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--c5-shard", default="split", choices=["split", "split-time", "symbols"],
@@ -441,16 +442,18 @@ class C5Batch(Workload):
             return x if (w0, nw) == (0, syms[sym][1]) else x[w0: w0 + nw - 1 + n].contiguous()
 
         lens = [syms[p[0]][0] for p in pieces]
-        if c5_mode == "group" and algo in ("auto", "slide"):
+        if c5_mode.startswith("group") and algo in ("auto", "slide"):
             self.series = [piece_series(*p) for p in pieces]
             self.outs = [torch.empty(p[2] * (n // 2), dtype=torch.float64, device=dev) for p, n in zip(pieces, lens)]
             self.group = bridge.Group(local_rank, lens, [p[2] for p in pieces])
+            if c5_mode == "group-per-length":
+                self.group.set_mode("per-length")
             if c5_streams:
                 self.group.set_streams(c5_streams)
             if slide_seg:
                 self.group.set_segment(slide_seg)
             self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
-            self.algorithm = "slide-group"
+            self.algorithm = "slide-group" + ("-per-length" if c5_mode == "group-per-length" else "")
             self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams or "library default",
                            "segment": slide_seg or "auto", "pieces": len(pieces)}
             self.windows = sum(p[2] for p in pieces)

@@ -1109,6 +1109,12 @@ struct Group {
     std::vector<int64_t> launch_bytes;     // output bytes per launch: what the slide's time follows
     std::mutex mu;                         // executes on the internal streams are enqueued one at a time
     int64_t seg = 0;                       // windows per workgroup, 0 = the launcher's policy
+    // one mixed-length persistent launch (slide_mixed.hip) when every member is 512..4096 with <= 3 window terms
+    // and there are at most kMixMax members; wsp_group_set_mode(1) forces the per-length launches
+    bool mix_ok = false;
+    int mode = 0;
+    int *ctr = nullptr;                    // 256 task-counter slots (counter, done) on the device, zeroed at create
+    uint32_t exec_no = 0;
     // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;  // [0] fork, [k] join of internal stream k - 1
@@ -1122,7 +1128,14 @@ struct Group {
         streams.clear();
         events.clear();
     }
-    ~Group() { release(); }
+    ~Group() {
+        release();
+        if (ctr) {
+            (void)hipSetDevice(dev);
+            (void)hipDeviceSynchronize();  // a queued execute may still count on its slot
+            (void)hipFree(ctr);
+        }
+    }
 };
 std::mutex g_groups_mu;
 std::map<int64_t, std::shared_ptr<Group>> *g_groups = new std::map<int64_t, std::shared_ptr<Group>>();
@@ -1134,6 +1147,80 @@ std::shared_ptr<Group> find_group(int64_t id) {
 }
 
 // (under g.mu) n lanes for wsp_group_execute: the caller's stream + n - 1 internal streams and their events
+constexpr int kMixSlots = 256;  // counter slots: executes of one group in flight at once on different streams
+
+// One persistent launch over every member (slide_mixed.hip), on the caller's stream.  Members are laid out class by
+// class, longest windows first; segment length S over the whole batch: about two tasks per resident workgroup (a task
+// = S windows x 2048 bins, half that for N <= 1024), 32..256 windows (wsp_group_set_segment overrides it).
+int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_out, hipStream_t s) {
+    const int n = (int)g.cfg.size();
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
+    SlideMix m{};
+    const Config &c0 = g.cfg[order[0]];
+    const int nf = window_coef(c0.window).nf;
+    const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
+    const int res = slide_mix_resident(nf, det, c0.f32, g.dev);
+    int64_t bins = 0;
+    for (const Config &c : g.cfg) bins += c.n_windows * (int64_t)(c.n / 2);
+    int64_t S = g.seg;
+    if (S <= 0) {
+        S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
+        S = std::min<int64_t>(256, std::max<int64_t>(32, S));
+    }
+    Tables t4096;
+    int st = get_tables(g.dev, 12, false, &t4096);
+    if (st != MTB_OK) return st;
+    m.tw4096 = t4096.tw;
+    int nc = -1, prev = -1;
+    int64_t tasks = 0, segs = 0;
+    auto close_class = [&]() {
+        if (nc < 0) return;
+        const int l2 = m.log2n[nc];
+        const int P = kMixNT * 2 * (l2 <= 10 ? 2 : 4) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
+        m.nseg[nc] = (int)segs;
+        m.task0[nc] = (int)tasks;
+        tasks += (segs + P - 1) / P;
+    };
+    for (int i = 0; i < n; ++i) {
+        const Config &c = g.cfg[order[i]];
+        if (c.log2n != prev) {
+            close_class();
+            ++nc;
+            prev = c.log2n;
+            SlideArgs A{};
+            if ((st = slide_args(g.dev, c, &A)) != MTB_OK) return st;
+            m.log2n[nc] = c.log2n;
+            m.seg[nc] = (int)S;
+            m.mem0[nc] = i;
+            m.c1[nc] = A.c1, m.sn1[nc] = A.sn1, m.c2[nc] = A.c2, m.sn2[nc] = A.sn2, m.inv_n[nc] = A.inv_n;
+            m.omega[nc] = A.omega;
+            m.s0 = A.s0, m.s1 = A.s1, m.s2 = A.s2;
+            segs = 0;
+        }
+        m.sg0[i] = segs;
+        m.n_windows[i] = c.n_windows;
+        m.series[i] = d_series[order[i]];
+        m.out[i] = d_out[order[i]];
+        segs += (c.n_windows + S - 1) / S;
+    }
+    close_class();
+    m.nclass = nc + 1;
+    m.mem0[m.nclass] = n;
+    if (tasks > INT32_MAX) {
+        set_error("wsp_group_execute: %lld tasks", (long long)tasks);
+        return MTB_BAD_ARGS;
+    }
+    m.n_tasks = (int)tasks;
+    const int slot = (int)(g.exec_no++ % kMixSlots);
+    m.counter = g.ctr + 2 * slot;
+    m.done = g.ctr + 2 * slot + 1;
+    const int grid = (int)std::min<int64_t>(res, tasks);
+    HIP_OR(launch_slide_mix(m, nf, det, c0.f32, grid, s), MTB_INTERNAL_ERROR);
+    return MTB_OK;
+}
+
 int group_lanes(Group &g, int n_streams) {
     g.release();
     if (n_streams == 1) return MTB_OK;
@@ -1846,7 +1933,17 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
             for (int m : g->launch.back()) b += g->cfg[m].n_windows * g->cfg[m].record() * (int64_t)g->cfg[m].elem();
             g->launch_bytes.push_back(b);
         }
-    // by default the launches run side by side, one lane each, up to 4 lanes (the HIP hardware queues a
+    g->mix_ok = (int)g->cfg.size() <= kMixMax;
+    for (const Config &c : g->cfg)
+        g->mix_ok = g->mix_ok && c.log2n >= 9 && c.log2n <= 12 && window_coef(c.window).nf <= 3;
+    if (g->mix_ok) {
+        if (hipSetDevice(device) != hipSuccess || hipMalloc(&g->ctr, 2 * kMixSlots * sizeof(int)) != hipSuccess ||
+            hipMemset(g->ctr, 0, 2 * kMixSlots * sizeof(int)) != hipSuccess) {
+            set_error("wsp_group_create: task counters could not be allocated");
+            return 0;
+        }
+    }
+    // per-length form: the launches run side by side, one lane each, up to 4 lanes (the HIP hardware queues a
     // process gets): C5 0.705-0.709 -> 0.669-0.671 ms against one lane (profiles/r03/s2/c5_lanes.log)
     {
         std::lock_guard<std::mutex> glk(g->mu);
@@ -1876,6 +1973,10 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
         }
     std::lock_guard<std::mutex> lk(g->mu);
     const hipStream_t caller = (hipStream_t)hip_stream;
+    if (g->mix_ok && g->mode == 0) {
+        HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
+        return group_execute_mixed(*g, d_series, d_out, caller);
+    }
     // wsp_group_set_streams(n > 1): the launches run side by side on n lanes -- the caller's stream and n - 1
     // internal streams (n HIP hardware queues in all) -- assigned greedily by output bytes, longest first, and
     // each lane's launches sized for the lane's share of the resident workgroup slots (its bytes / all bytes),
@@ -1952,7 +2053,20 @@ MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group) {
 
 MTB_API int32_t wsp_group_launches(int64_t group) {
     std::shared_ptr<Group> g = find_group(group);
-    return g ? (int32_t)g->launch.size() : -1;
+    if (!g) return -1;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return g->mix_ok && g->mode == 0 ? 1 : (int32_t)g->launch.size();
+}
+
+MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g || mode < 0 || mode > 1) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..1", (long long)group, mode);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->mode = mode;
+    return MTB_OK;
 }
 
 MTB_API int32_t wsp_group_destroy(int64_t group) {

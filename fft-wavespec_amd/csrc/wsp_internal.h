@@ -147,6 +147,34 @@ struct SlideGroup {
     int64_t blk0[kSlideGroupMax + 1];  // filled by the launcher
 };
 hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream_t stream);
+// Mixed-length grouped launch (slide_mixed.hip): the members of a group of window lengths 512 .. 4096 in ONE
+// persistent launch.  A 512-thread workgroup takes tasks from a device counter; a task is one segment of a
+// 4096-pt member, or 512 / NT(N) segments of a shorter length side by side (2 x 2048, 2 x 1024, 4 x 512: one
+// sub-workgroup of NT = N / (2 B) threads each).  Tasks run longest windows first, so the four lengths' seed
+// phases and drains overlap instead of each launch paying its own.  Members are laid out class by class
+// (class c = one window length, longest first); series / out are the caller's pointers of this execute.
+constexpr int kMixMax = 32;    // members per mixed launch
+constexpr int kMixClass = 4;   // window lengths 4096, 2048, 1024, 512
+constexpr int kMixNT = 512;    // threads per workgroup
+struct SlideMix {
+    int nclass, n_tasks;
+    int log2n[kMixClass], seg[kMixClass];
+    int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
+    double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];
+    double s0, s1, s2;                  // a0, a1/2, a2/2 of the (common) window
+    const void *omega[kMixClass];       // slide table of class c (SlideArgs::omega)
+    const void *tw4096;                 // W_4096^k, double complex: the quarter table of every length
+    int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup)
+    int64_t sg0[kMixMax];               // member i: its first segment within its class
+    int64_t n_windows[kMixMax];
+    const void *series[kMixMax];
+    void *out[kMixMax];
+};
+// One launch of `grid` persistent workgroups (grid <= the resident count, slide_mix_resident).
+hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t stream);
+// Resident 512-thread workgroups of the mixed kernel on device `dev` (occupancy x CUs).
+int slide_mix_resident(int nf, int detrend, bool f32, int dev);
+
 // hop = 1 top-k records ([bin, power, Re, Im] x topk per window, MTB_OUT_TOPK) by the sliding DFT: the
 // band's trackers only (span <= 512), one wave per segment, the FFT kernel's one-wave scan per window.
 constexpr int kSlideTopkMaxSpan = 512;

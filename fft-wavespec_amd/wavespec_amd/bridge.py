@@ -82,6 +82,7 @@ SIGNATURES = {
     "wsp_group_launches": (C.c_int32, [C.c_int64]),
     "wsp_group_set_streams": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_group_set_segment": (C.c_int32, [C.c_int64, C.c_int64]),
+    "wsp_group_set_mode": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_group_destroy": (C.c_int32, [C.c_int64]),
     "wsp_version": (C.c_char_p, []),
 }
@@ -381,6 +382,12 @@ class Group:
     def set_segment(self, windows: int) -> None:
         """Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy)."""
         _check("wsp_group_set_segment", lib().wsp_group_set_segment(self.handle, windows))
+
+    MODES = {"auto": 0, "per-length": 1}
+
+    def set_mode(self, mode: str) -> None:
+        """"auto": one mixed-length persistent launch where eligible; "per-length": one launch per window length."""
+        _check("wsp_group_set_mode", lib().wsp_group_set_mode(self.handle, self.MODES[mode]))
 
     def execute(self, d_series, d_out, stream: int = 0) -> None:
         """d_series / d_out: device pointers (ints), one per member."""

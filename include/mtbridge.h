@@ -331,9 +331,10 @@ MTB_API int64_t wsp_plan_algorithmic_bytes(int64_t plan);
  * shape (one series per symbol, WaveCyclesBatchFetcher.mq5:112-118; C5 = 28
  * symbols x 4 window lengths) on device-resident buffers.  Member m: a series
  * of n_windows[m] + window_len[m] - 1 samples, every window of it (hop = 1),
- * MTB_OUT_POWER rows of window_len[m]/2 elements.  The members of each window
- * length run in one sliding-DFT launch (longest windows first, up to 16
- * members per launch), segmented over the length's total window count.
+ * MTB_OUT_POWER rows of window_len[m]/2 elements.  All members run in one
+ * persistent sliding-DFT launch (wsp_group_set_mode), or the members of each
+ * window length in one launch (longest windows first, up to 16 members per
+ * launch), segmented over the length's total window count.
  * Members must be sliding-DFT batches: window_len 512..8192, detrend none or
  * mean, Hann / Hamming / Blackman / no window (Blackman up to 4096).  Returns
  * a handle > 0, or 0 (see gpu_get_last_error_w). */
@@ -350,7 +351,8 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
 MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, void *const *d_out, void *hip_stream);
 /* Algorithmic bytes of one execute (sum over members, as wsp_plan_algorithmic_bytes). */
 MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
-/* Kernel launches one execute makes (one per window length and 16 members). */
+/* Kernel launches one execute makes: 1 for the mixed-length launch, else one
+ * per window length and 16 members. */
 MTB_API int32_t wsp_group_launches(int64_t group);
 /* Tuning: n_streams > 1 runs every execute's launches side by side on n
  * lanes -- the caller's stream and n - 1 internal streams forked from it and
@@ -364,6 +366,14 @@ MTB_API int32_t wsp_group_set_streams(int64_t group, int32_t n_streams);
 /* Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy over
  * each window length's total window count), at most 2048. */
 MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
+/* Tuning / ablation: 0 (default) = the library's choice -- ONE persistent
+ * launch over every member when all window lengths are 512..4096, the window
+ * has at most three cosine terms (none / Hann / Hamming) and there are at
+ * most 32 members (workgroups pull segments of all lengths from a device
+ * counter, longest windows first); otherwise one launch per window length.
+ * 1 = one launch per window length (lanes: wsp_group_set_streams).
+ * MTB_BAD_ARGS outside 0..1. */
+MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
 MTB_API int32_t wsp_plan_destroy(int64_t plan);

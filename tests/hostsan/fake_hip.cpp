@@ -178,6 +178,10 @@ hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
     memcpy(d, s, n);
     return hipSuccess;
 }
+hipError_t hipMemset(void *d, int v, size_t n) {
+    memset(d, v, n);
+    return hipSuccess;
+}
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t st) {
     check_op(st, {d, s});
     run_on(st, [=] { memcpy(d, s, n); });
@@ -329,6 +333,27 @@ hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream
         for (int m = 0; m < gg.n; ++m) {
             if (c.f32) fill<float>(gg.series[m], 1, n, gg.n_windows[m], n / 2, gg.out[m]);
             else fill<double>(gg.series[m], 1, n, gg.n_windows[m], n / 2, gg.out[m]);
+        }
+    });
+    return hipSuccess;
+}
+int slide_mix_resident(int, int, bool, int) { return 512; }
+hipError_t launch_slide_mix(const SlideMix &m, int, int, bool f32, int grid, hipStream_t s) {  // every member, same records
+    if (grid < 1 || m.nclass < 1 || m.n_tasks < 1 || !m.counter || !m.done) return hipErrorInvalidValue;
+    int64_t total = 0;
+    for (int i = 0; i < m.mem0[m.nclass]; ++i) {
+        check_op(s, {m.series[i], m.out[i]});
+        total += m.n_windows[i];
+    }
+    check_op(s, {}, total);
+    const SlideMix c = m;
+    run_on(s, [c, f32] {
+        for (int k = 0; k < c.nclass; ++k) {
+            const int n = 1 << c.log2n[k];
+            for (int i = c.mem0[k]; i < c.mem0[k + 1]; ++i) {
+                if (f32) fill<float>(c.series[i], 1, n, c.n_windows[i], n / 2, c.out[i]);
+                else fill<double>(c.series[i], 1, n, c.n_windows[i], n / 2, c.out[i]);
+            }
         }
     });
     return hipSuccess;

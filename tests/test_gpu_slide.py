@@ -451,12 +451,14 @@ def test_stateful_plan_on_two_streams(gpu_session, kind):
     plan.close()
 
 
+@pytest.mark.parametrize("mode", ["auto", "per-length"])
 @pytest.mark.parametrize("prec,detrend,window", [("f64", "none", "hann"), ("f64", "mean", "blackman"),
                                                  ("f32", "mean", "hamming"), ("f64", "none", "none")])
-def test_group_mixed_members(gpu_session, prec, detrend, window):
+def test_group_mixed_members(gpu_session, prec, detrend, window, mode):
     """Grouped hop = 1 plan (wsp_group_*) with mixed window lengths, more than 16 members of one length
-    (two launches for it), a one-window member and members shorter than a segment: every window of every
-    member against the oracle."""
+    (two launches for it in the per-length form), a one-window member and members shorter than a segment:
+    every window of every member against the oracle -- through the one mixed-length persistent launch
+    (mode auto; Blackman's five window terms take the per-length launches) and the per-length launches."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     lens = [512] * 18 + [1024, 2048, 4096, 1024, 512]
@@ -466,7 +468,9 @@ def test_group_mixed_members(gpu_session, prec, detrend, window):
     series = [torch.from_numpy(h).to(dev, tdt) for h in hs]
     outs = [torch.empty(nw * (n // 2), dtype=tdt, device=dev) for n, nw in zip(lens, nwins)]
     g = bridge.Group(0, lens, nwins, detrend, window, prec)
-    assert g.launches == 2 + 3  # 512: 19 members in two launches; 1024, 2048, 4096 one each
+    g.set_mode(mode)
+    mixed = mode == "auto" and window != "blackman"
+    assert g.launches == (1 if mixed else 2 + 3)  # per length: 512's 19 members in two launches; 1024, 2048, 4096
     g.execute([x.data_ptr() for x in series], [o.data_ptr() for o in outs], torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     tol = 1e-5 if prec == "f32" else 1e-10
@@ -492,6 +496,7 @@ def test_group_lanes(gpu_session, lanes):
     series = [torch.from_numpy(h).to(dev) for h in hs]
     outs = [torch.empty(nw * (n // 2), dtype=torch.float64, device=dev) for n, nw in zip(lens, nwins)]
     g = bridge.Group(0, lens, nwins)
+    g.set_mode("per-length")  # the lanes carry the per-length launches
     g.set_streams(lanes)
     ptrs = ([x.data_ptr() for x in series], [o.data_ptr() for o in outs])
     g.execute(*ptrs, torch.cuda.current_stream().cuda_stream)
@@ -505,6 +510,79 @@ def test_group_lanes(gpu_session, lanes):
         want = oracle.batch_spectrum(hs[i], n, 1, "none", "hann")
         assert oracle.rel_err(got.reshape(nw, n // 2), want) <= 1e-10, (i, n, nw)
     g.close()
+
+
+@pytest.mark.parametrize("seg", [0, 7, 333, 2048])
+def test_group_mixed_launch(gpu_session, seg):
+    """The mixed-length persistent launch (slide_mixed.hip): C5's four lengths with ragged members, segments of the
+    policy / 7 / 333 / 2048 windows (sub-workgroups of a task running segments of different lengths and past a
+    class's end), every window against the oracle; executes repeated on the same stream (the task-counter slot is
+    reset by the kernel's last workgroup) and two executes at once on two streams with other buffers (two counter
+    slots) are identical to the first."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    lens = [512, 1024, 2048, 4096, 512, 4096, 2048, 1024, 512, 512, 2048]
+    nwins = [2500, 1900, 1300, 700, 3, 1, 333, 2048, 777, 64, 1]
+    hs = [synth.random_walk(nw + n - 1, seed=500 + i) for i, (n, nw) in enumerate(zip(lens, nwins))]
+    series = [torch.from_numpy(h).to(dev) for h in hs]
+    mk = lambda: [torch.empty(nw * (n // 2), dtype=torch.float64, device=dev) for n, nw in zip(lens, nwins)]
+    outs, outs2 = mk(), mk()
+    g = bridge.Group(0, lens, nwins)
+    assert g.launches == 1
+    if seg:
+        g.set_segment(seg)
+    sp = [x.data_ptr() for x in series]
+    st = torch.cuda.current_stream().cuda_stream
+    g.execute(sp, [o.data_ptr() for o in outs], st)
+    torch.cuda.synchronize()
+    first = [o.cpu().numpy().copy() for o in outs]
+    for i, (n, nw) in enumerate(zip(lens, nwins)):
+        want = oracle.batch_spectrum(hs[i], n, 1, "none", "hann")
+        assert oracle.rel_err(first[i].reshape(nw, n // 2), want) <= 1e-10, (i, n, nw)
+        kmin, kmax = oracle.band(n)
+        assert oracle.inband_err(first[i].reshape(nw, n // 2), want, kmin, kmax) <= 1e-10, (i, n, nw)
+    for _ in range(3):
+        g.execute(sp, [o.data_ptr() for o in outs], st)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    g.execute(sp, [o.data_ptr() for o in outs2], s1.cuda_stream)
+    g.execute(sp, [o.data_ptr() for o in outs], s2.cuda_stream)
+    torch.cuda.synchronize()
+    for i in range(len(lens)):
+        assert np.array_equal(outs[i].cpu().numpy(), first[i]), i
+        assert np.array_equal(outs2[i].cpu().numpy(), first[i]), i
+    g.close()
+
+
+def test_group_mixed_vs_per_length_c5(gpu_session):
+    """C5's 28 symbols (20000 bars, N = 512 .. 4096 by sevens): the mixed-length launch against the per-length
+    launches on the same buffers, every window (the two forms seed at different windows, so they agree to the
+    parity bar, not bit for bit), and the oracle on sampled windows of every symbol."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    lens = [(512, 1024, 2048, 4096)[s // 7] for s in range(28)]
+    nwins = [20000 - n + 1 for n in lens]
+    series = [synth.random_walk_torch(20000, 100 + s, dev) for s in range(28)]
+    res = {}
+    for mode in ("auto", "per-length"):
+        outs = [torch.empty(nw * (n // 2), dtype=torch.float64, device=dev) for n, nw in zip(lens, nwins)]
+        g = bridge.Group(0, lens, nwins)
+        g.set_mode(mode)
+        g.execute([x.data_ptr() for x in series], [o.data_ptr() for o in outs], torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        g.close()
+        res[mode] = outs
+    rng = np.random.default_rng(9)
+    for s in range(28):
+        n, nw = lens[s], nwins[s]
+        A, B = res["auto"][s].view(nw, n // 2), res["per-length"][s].view(nw, n // 2)
+        rel = ((A - B).abs().max(dim=1).values / B.max(dim=1).values).max().item()
+        assert rel <= 1e-10, (s, rel)
+        idx = np.unique(np.r_[0, nw - 1, rng.integers(0, nw, 6)])
+        h = series[s].cpu().numpy()
+        want = np.stack([oracle.window_spectrum(h[i:i + n], "none", "hann") for i in idx])
+        got = A[torch.from_numpy(idx).to(dev)].cpu().numpy()
+        assert oracle.rel_err(got, want) <= 1e-10, s
 
 
 def test_group_refusals(gpu_session):
