@@ -613,6 +613,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
     L.topk = c.topk;
     L.kmin = c.kmin;
     L.kmax = c.kmax;
+    L.variant = c.output == MTB_OUT_TOPK_PHASE ? c.variant : 0;
     if (L.detrend == kDetrendIir) {
         // L/WaveSpecZZ_1.0.2.mq5:3041-3043, same double expressions as the CPU path
         const double omega = 2.0 * M_PI / c.trend_period;

@@ -495,9 +495,11 @@ __device__ __forceinline__ int wave_min64(int b) {
 // that max (scalar find-first, no second reduction chain); only a tie between lanes (equal powers)
 // takes the min-over-bins reduction.  Lane r keeps round r's winner; lanes < k write the records
 // at the end (one contiguous 4k-element row).
-template <int NB, typename T>
+// RW: record width (4; 6 for kOutTopKPhase, whose fields 4-5 the caller adds); *slot_bin (optional): the bin of
+// this lane's slot, -1 when empty.
+template <int NB, typename T, int RW = 4>
 __device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span, int k, int lane, T *rec, bool active,
-                                            int *winners = nullptr) {
+                                            int *winners = nullptr, int *slot_bin = nullptr) {
     // the lane's NB candidates sorted once (power desc, bin asc): its best is always p[0] and
     // retiring it is a shift, not a rescan
     T p[NB];
@@ -583,8 +585,9 @@ __device__ __forceinline__ void topk_wave64(const cpx<T> *xb, int kmin, int span
         }
     }
     if (winners && lane < k) winners[lane] = my_j;  // band index of slot `lane`, -1 when empty
+    if (slot_bin) *slot_bin = my_j >= 0 ? kmin + my_j : -1;
     if (active && lane < k) {
-        T *o = rec + 4 * lane;
+        T *o = rec + RW * lane;
         if (my_j >= 0) {
             const cpx<T> x = xb[my_j];
             o[0] = T(kmin + my_j);
@@ -706,6 +709,90 @@ __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, doub
         if (g > 100.0) g = 100.0;
         if (g < -100.0) g = -100.0;
         gd[j] = g;
+    }
+}
+
+// The unwrap's correction between consecutive bins (UnwrapPhase, L/WaveSpecZZ_1.0.4-new.mq5:1068-1077): -1 when
+// atan2(B) - atan2(A) > pi, +1 when < -pi, else 0 -- decided from the half-planes and the cross product
+// cross(A, B) = |A||B| sin(phi_B - phi_A) instead of two atan2: with both imaginary parts non-zero, a jump above
+// pi needs phi_A < 0 < phi_B and sin < 0 (below -pi: phi_A > 0 > phi_B and sin > 0).  Where that test is not
+// clear-cut -- an exactly zero imaginary part (the +-0 / +-pi conventions of atan2) or |sin| <= 1e-12, i.e.
+// within 1e-12 rad of the tie, far beyond the few ulps by which the computed atan2 difference can be off --
+// the decision is taken from the atan2 values themselves, so it is the one phase_chunk takes in every case.
+__device__ __noinline__ int unwrap_corr_atan2(double ax, double ay, double bx, double by) {  // the rare path: a call
+    constexpr double kPi = 3.14159265358979323846;
+    const double diff = atan2(by, bx) - atan2(ay, ax);
+    return diff > kPi ? -1 : diff < -kPi ? 1 : 0;
+}
+__device__ __forceinline__ int unwrap_corr(cpx<double> A, cpx<double> B) {
+    const double ya = A.im, yb = B.im;
+    if (ya != 0.0 && yb != 0.0) {
+        if ((ya < 0.0) == (yb < 0.0)) return 0;  // same open half-plane: |diff| < pi
+        const double cr = A.re * B.im - A.im * B.re;
+        const double na = A.re * A.re + A.im * A.im, nb = B.re * B.re + B.im * B.im;
+        if (cr * cr > 1e-24 * na * nb) return ya < 0.0 ? (cr < 0.0 ? -1 : 0) : (cr > 0.0 ? 1 : 0);
+    }
+    return unwrap_corr_atan2(A.re, A.im, B.re, B.im);
+}
+
+// [unwrapped phase, group delay] of the top-k winners by ONE wave (kOutTopKPhase on the split exchange), the values
+// phase_chunk gives them: bins 0 .. kmax + 1 are staged at xrow[k] (bin M, the zeroed upper half, reads as 0).
+// Lane l holds the corrections into bins [CH l, CH l + CH] as two bit masks (unwrap_corr: no atan2 but at near
+// ties), the count before its chunk is an exact wave prefix sum, and atan2 runs only for each winner and its two
+// neighbours (lane s: slot s, `bin` its bin or -1): u = phi + 2 pi K (the same fma), delay -(u[b+1] - u[b-1]) / 2
+// (bin 0: -(u[1] - u[0])), clamped to +-100 (L/WaveSpecZZ_1.0.4-new.mq5:1102-1119).  64 CH >= kmax + 2.
+template <int CH>
+__device__ __forceinline__ void topk_phase_wave(const cpx<double> *xrow, int M, int kmax, int k, int lane, int bin, double *rec,
+                                                bool active) {
+    constexpr double k2Pi = 2.0 * 3.14159265358979323846;
+    static_assert(CH <= 16, "two 32-bit correction masks per lane");
+    const int top = kmax + 1;  // highest bin any winner's unwrapped phase or delay reads
+    auto X = [&](int kk) { return kk < M && kk <= top ? xrow[kk] : cpx<double>{0.0, 0.0}; };
+    const int k0 = CH * lane;
+    unsigned pos = 0u, neg = 0u;  // bit j: the correction into bin k0 + j is +1 / -1 (j = CH: the next chunk's first)
+    cpx<double> prev = k0 > 0 ? X(k0 - 1) : cpx<double>{0.0, 0.0};
+#pragma unroll 1
+    for (int j = 0; j <= CH; ++j) {
+        const int kk = k0 + j;
+        if (kk > top) break;  // bins past kmax + 1 feed no winner
+        const cpx<double> cur = X(kk);
+        const int c = kk == 0 ? 0 : unwrap_corr(prev, cur);
+        pos |= (c > 0 ? 1u : 0u) << j;
+        neg |= (c < 0 ? 1u : 0u) << j;
+        prev = cur;
+    }
+    const unsigned own = (1u << CH) - 1u;
+    const int sum = __popc(pos & own) - __popc(neg & own);
+    int incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int up = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += up;
+    }
+    const int K = incl - sum;  // corrections of every bin < k0
+    const int b = bin >= 0 ? bin : 0;
+    double um = 0.0, u0 = 0.0, up = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < 3; ++i) {  // u[b - 1], u[b], u[b + 1] (one atan2 in the code); every lane takes part
+        const int bb = b - 1 + i < 0 ? 0 : b - 1 + i;
+        const int ob = bb / CH < 64 ? bb / CH : 63, jb = bb - CH * ob;
+        const int Ko = __shfl(K, ob, 64);
+        const unsigned po = (unsigned)__shfl((int)pos, ob, 64), no = (unsigned)__shfl((int)neg, ob, 64);
+        const unsigned m = jb >= 31 ? 0xffffffffu : (2u << jb) - 1u;
+        const int Kb = Ko + __popc(po & m) - __popc(no & m);
+        const cpx<double> x = X(bb);
+        const double uu = fma((double)Kb, k2Pi, bb < M ? atan2(x.im, x.re) : 0.0);
+        um = i == 0 ? uu : um;
+        u0 = i == 1 ? uu : u0;
+        up = i == 2 ? uu : up;
+    }
+    const double u3[3] = {um, u0, up};
+    double g = b == 0 ? -(u3[2] - u3[1]) : -(u3[2] - u3[0]) / 2.0;
+    if (g > 100.0) g = 100.0;
+    if (g < -100.0) g = -100.0;
+    if (active && lane < k) {
+        rec[6 * lane + 4] = bin >= 0 ? u3[1] : 0.0;
+        rec[6 * lane + 5] = bin >= 0 ? g : 0.0;
     }
 }
 
@@ -1077,6 +1164,10 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
                 if ((unsigned)(ka - a.kmin) <= (unsigned)(a.kmax - a.kmin)) xrow[ka - a.kmin] = {kS1 * xa.re, kS1 * xa.im};
                 if ((unsigned)(kb - a.kmin) <= (unsigned)(a.kmax - a.kmin)) xrow[kb - a.kmin] = {kS1 * xb.re, kS1 * xb.im};
+            } else if constexpr (OUT == kOutTopKPhase && kSplit) {  // stage X[0 .. kmax + 1] (split slot)
+                cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
+                if ((unsigned)ka <= (unsigned)(a.kmax + 1)) xrow[ka] = {kS1 * xa.re, kS1 * xa.im};
+                if ((unsigned)kb <= (unsigned)(a.kmax + 1)) xrow[kb] = {kS1 * xb.re, kS1 * xb.im};
             } else if constexpr (kPhase) {  // stage X for the phase / scan (AoS slot)
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
                 xrow[pad16(ka)] = {kS1 * xa.re, kS1 * xa.im};
@@ -1158,6 +1249,28 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                     }
                     continue;  // next group (its first exchange barrier orders this scan's LDS reads)
                 }
+            }
+            if constexpr (OUT == kOutTopKPhase && TPW >= 64 && (VAR & kVarSplitLds)) {
+                // the split-exchange form (the host checks that bins 0 .. kmax + 1 fit the slot and the band holds
+                // at most 8 bins per lane): one wave scans the band, then the same wave adds the winners' unwrapped
+                // phase and group delay (topk_phase_wave) -- 3 waves per SIMD instead of the AoS form's 2
+                if (t < 64) {
+                    const cpx<T> *xb = xrow + a.kmin;
+                    const int nb = (span + 63) / 64;
+                    int bin = -1;
+                    if (nb <= 1) topk_wave64<1, T, 6>(xb, a.kmin, span, a.topk, t, recw, active, nullptr, &bin);
+                    else if (nb <= 2) topk_wave64<2, T, 6>(xb, a.kmin, span, a.topk, t, recw, active, nullptr, &bin);
+                    else if (nb <= 4) topk_wave64<4, T, 6>(xb, a.kmin, span, a.topk, t, recw, active, nullptr, &bin);
+                    else topk_wave64<8, T, 6>(xb, a.kmin, span, a.topk, t, recw, active, nullptr, &bin);
+                    const int need = a.kmax + 2;
+                    const cpx<double> *xd = reinterpret_cast<const cpx<double> *>(xrow);
+                    double *rd = reinterpret_cast<double *>(recw);
+                    if (need <= 128) topk_phase_wave<2>(xd, M, a.kmax, a.topk, t, bin, rd, active);
+                    else if (need <= 256) topk_phase_wave<4>(xd, M, a.kmax, a.topk, t, bin, rd, active);
+                    else if (need <= 512) topk_phase_wave<8>(xd, M, a.kmax, a.topk, t, bin, rd, active);
+                    else topk_phase_wave<16>(xd, M, a.kmax, a.topk, t, bin, rd, active);
+                }
+                continue;  // next group (its first exchange barrier orders this wave's LDS reads)
             }
             if constexpr (!(OUT == kOutTopK && TPW >= 64 && (VAR & kVarSplitLds))) {
             auto write_x = [&](T *rec, int b, T pw_) {

@@ -87,9 +87,13 @@ template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var
     // of the bins: dispatch_win falls back to the AoS slot for wider bands)
     // (top-k: the split exchange where one wave scans the band, N = 2048 / 4096 without detrend;
     // elsewhere its scan paths spill at 168 VGPRs)
-    if constexpr (OUT == kOutTopK)
-        return (DETREND == kDetrendNone && (LOG2N == 11 || LOG2N == 12)) ? kDefaultVar : kCommonVar;
-    return (OUT == kOutPhase || OUT == kOutTopKPhase) ? (kVarNoPrefetch | kVarNtStore)
+    // (top-k + phase: the same split-exchange one-wave scan, then one wave for the winners' phases, round 4;
+    // dispatch_win falls back to the AoS form when bins 0 .. kmax + 1 do not fit the split slot)
+    if constexpr (OUT == kOutTopK || OUT == kOutTopKPhase)
+        return (DETREND == kDetrendNone && (LOG2N == 11 || LOG2N == 12)) ? kDefaultVar
+               : OUT == kOutTopK                                          ? kCommonVar
+                                                                          : (kVarNoPrefetch | kVarNtStore);
+    return (OUT == kOutPhase) ? (kVarNoPrefetch | kVarNtStore)
            : (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
                ? kCommonVar
                : kDefaultVar;
@@ -99,6 +103,12 @@ template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var
 template <typename T, int LOG2N, int VAR> constexpr bool band_fits(int span) {
     return !(VAR & kVarSplitLds) ||
            (span <= 64 * 8 && (int64_t)span * (int64_t)sizeof(cpx<T>) <= (int64_t)Geo<LOG2N>::SLOT * (int64_t)sizeof(T));
+}
+// The split-exchange top-k + phase form stages bins 0 .. kmax + 1 and its phase wave covers 64 x 16 bins.
+template <typename T, int LOG2N, int VAR> constexpr bool phase_prefix_fits(int kmax, int span) {
+    return !(VAR & kVarSplitLds) ||
+           (span <= 64 * 8 && kmax + 2 <= 64 * 16 &&
+            (int64_t)(kmax + 2) * (int64_t)sizeof(cpx<T>) <= (int64_t)Geo<LOG2N>::SLOT * (int64_t)sizeof(T));
 }
 
 // Non-temporal sample loads as a compile-time variant (kVarNtLoad) where the windows do not overlap:
@@ -129,6 +139,17 @@ hipError_t launch_one(const SpectrumLaunch &L, hipStream_t stream) {
 template <typename T, int LOG2N, int DETREND, int OUT>
 hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
     double a0, a1, a2;
+    if constexpr (OUT == kOutTopKPhase && (default_var<T, LOG2N, DETREND, OUT>() & kVarSplitLds) != 0) {
+        constexpr int kAos = kVarNoPrefetch | kVarNtStore;
+        if (L.variant == 1 || !phase_prefix_fits<T, LOG2N, default_var<T, LOG2N, DETREND, OUT>()>(L.kmax, L.kmax - L.kmin + 1)) {
+            switch (window_class(L.window, &a0, &a1, &a2)) {
+            case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos, kAos>(L, s);
+            case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2, kAos>(L, s);
+            case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett, kAos>(L, s);
+            default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone, kAos>(L, s);
+            }
+        }
+    }
     if constexpr (OUT == kOutTopK && (default_var<T, LOG2N, DETREND, OUT>() & kVarSplitLds) != 0) {
         if (!band_fits<T, LOG2N, default_var<T, LOG2N, DETREND, OUT>()>(L.kmax - L.kmin + 1)) {
             switch (window_class(L.window, &a0, &a1, &a2)) {

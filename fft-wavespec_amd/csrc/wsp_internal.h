@@ -38,6 +38,7 @@ struct SpectrumLaunch {
     int grid;             // 0 = auto
     int nt_mode;          // non-temporal sample loads: 0 = auto (hop >= N), 1 = off, 2 = on
     int vec_mode;         // pair loads: 0 = auto (aligned only), 1 = scalar, 2 = vector even if unaligned
+    int variant;          // wsp_plan_set_variant: kOutTopKPhase 1 = the AoS form (ablation)
 };
 
 hipError_t launch_spectrum(const SpectrumLaunch &L, hipStream_t stream);

@@ -311,7 +311,10 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    N = 65536); 4 = its 256-thread form with register prefetch; 5 = the fused
  *    kernel with plain (not non-temporal) output stores;
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
- *    one-lane-per-window filter. */
+ *    one-lane-per-window filter;
+ *  - MTB_OUT_TOPK_PHASE records (FFT kernel): 1 = the AoS form (two waves per
+ *    SIMD, every thread's phase chunk) instead of the split-exchange one-wave
+ *    scan + one-wave winners' phases. */
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);
 /* Diagnostics: d_flags (device, n_windows bytes, or NULL = off) receives, on
  * every execute of a hop = 1 top-k plan by the probe-threshold scan (variant

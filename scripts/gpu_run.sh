@@ -12,7 +12,8 @@
 #   bench=<cfg>[,<args>]     python bench.py --config <cfg> --steps 100 --warmup 20 --no-cpu-baseline <args>
 #                            (args comma-separated), line bench_<cfg>.json
 #   default                  python bench.py (the driver's default line, CPU baseline included)
-#   prof=<cfg>[,<algo>[,<variant>]] rocprofv3 kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own
+#   prof=<cfg>[,<algo>[,<variant>[,<key suffix>[,<extra bench args, + for spaces>]]]]
+#                            rocprofv3 kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own
 #                            passes (scripts/gpu_profile.sh), parsed by scripts/parse_prof.py
 #   sq=<cfg>,<counters>      one rocprofv3 --pmc pass with the given SQ_ counters (<= 8), sq_<cfg>.csv
 #   kbench=<args>            fft-wavespec_amd/bin/kbench <args> (spaces as commas)
@@ -73,8 +74,8 @@ print('$cfg', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g wi
         cat $O/bench_default.json
         ;;
     prof)
-        IFS=',' read -r cfg algo var <<< "$val"
-        run 900 $O/prof_$cfg.log $O/prof_$cfg.log bash scripts/gpu_profile.sh $TAG $cfg ${algo:-auto} ${var:-0}
+        IFS=',' read -r cfg algo var suf extra <<< "$val"
+        run 900 $O/prof_$cfg.log $O/prof_$cfg.log bash scripts/gpu_profile.sh $TAG $cfg ${algo:-auto} ${var:-0} "${suf:-}" ${extra//+/ }
         cat $O/prof_$cfg.log
         ;;
     sq)

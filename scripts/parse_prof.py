@@ -14,9 +14,9 @@ from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
 key = sys.argv[3] if len(sys.argv) > 3 else cfg  # e.g. c4_fft: the config under a forced algorithm
-OURS = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "slide_seed_kernel", "slide_seed_r_kernel", "fused_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
+OURS = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "slide_seed_kernel", "slide_seed_r_kernel", "fused_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
         "iir_kernel")
-MAIN = ("spectrum_kernel", "slide_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "inverse_kernel", "row_kernel",
+MAIN = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "inverse_kernel", "row_kernel",
         "fused_kernel")  # one per step; a Kalman pre-pass adds to its step
 
 
@@ -36,8 +36,8 @@ def main_per_step(cfg):
     """Main-kernel dispatches per bench step: 1, the chunk count of the four-step large-N path
     (one row_kernel per chunk of windows, csrc/large_fft.hip large_chunk: 192 MiB of column results),
     or C5's launches."""
-    if cfg == "c5":  # grouped plan: one slide launch per window length; per-symbol plans: 28 launches
-        return 28 if key.endswith(("_plans", "_fft")) else 4
+    if cfg == "c5":  # grouped plan: one mixed-length launch (per-length form: one per window length); per-symbol plans: 28
+        return 28 if key.endswith(("_plans", "_fft")) else (4 if key.endswith("_per_length") else 1)
     sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "fft-wavespec_amd"))
     from wavespec_amd import synth
     c = synth.CONFIGS.get(cfg)

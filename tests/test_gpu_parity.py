@@ -418,6 +418,46 @@ def test_topk_phase(gpu_session, n, hop, k, minp, maxp):
             assert np.max(np.abs(got[w, same, 4:] - want[w, same, 4:]), initial=0.0) <= 1e-8
 
 
+@pytest.mark.parametrize("n,k,minp,maxp,window", [(4096, 8, 18, 200, "hann"), (2048, 8, 18, 200, "hann"),
+                                                  (4096, 8, 6, 200, "hamming"), (4096, 5, 3, 300, "hann"),
+                                                  (2048, 8, 4.1, 2000, "none"), (4096, 64, 18, 200, "blackman"),
+                                                  (2048, 1, 9, 30, "hann"), (4096, 8, 100, 110, "hann")])
+def test_topk_phase_split_form(gpu_session, n, k, minp, maxp, window):
+    """MTB_OUT_TOPK_PHASE without detrend at N = 2048 / 4096 (ns_topk_phase's instantiation): the split-exchange
+    form (one-wave scan, then one wave for the winners' phases: geometric unwrap decisions, atan2 only at each
+    winner and its neighbours) against the AoS form (wsp_plan_set_variant 1: every thread's phase chunk) --
+    identical records, the same decisions and the same fma -- and against the oracle.  Bands whose bins
+    0 .. kmax + 1 take 2 / 4 / 8 / 16 bins per lane, and one beyond the split slot (periods 3-300: the AoS form)."""
+    torch = pytest.importorskip("torch")
+    nwin = 300
+    s = synth.random_walk(nwin * n, seed=n + k + 17)
+    dev = torch.device("cuda", 0)
+    d_s = torch.from_numpy(s).to(dev)
+    outs = []
+    for v in (0, 1):
+        plan = bridge.Plan(0, n, n, nwin, "none", window, output="topk_phase")
+        plan.set_topk(k, minp, maxp)
+        plan.set_variant(v)
+        d_o = torch.full((nwin * 6 * k,), float("nan"), dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(d_o.view(nwin, k, 6).cpu().numpy())
+        plan.close()
+    assert np.array_equal(outs[0], outs[1])
+    got = outs[0]
+    want = oracle.batch_topk_phase(s, n, n, "none", window, 0, None, k, minp, maxp)
+    _topk_match(got[:, :, :4], want[:, :, :4], 1e-10, ref(s, n, n, "none", window).max(axis=1))
+    full = oracle.batch_phase(s, n, n, "none", window)
+    for w in range(nwin):
+        mag = np.sqrt(full[w, 0])
+        ok = mag >= 1e-9 * mag.max()
+        same = (got[w, :, 0] == want[w, :, 0]) & (want[w, :, 0] >= 0)
+        b = want[w, same, 0].astype(int)
+        if ok[: max(b.max(initial=0), 1) + 2].all():
+            assert np.max(np.abs(got[w, same, 4:] - want[w, same, 4:]), initial=0.0) <= 1e-8
+        assert np.all(got[w, want[w, :, 0] < 0, 4:] == 0.0)
+
+
 @pytest.mark.parametrize("length", [2, 6, 64, 1000, 4096, 10002])
 @pytest.mark.parametrize("method", ["unwrapped", "wrapped", "group_delay"])
 def test_spectral_phase_unwrap(gpu_session, length, method):
