@@ -521,6 +521,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         I.twiddle = t.tw;
         I.n_windows = c.n_windows;
         I.log2n = c.log2n;
+        I.variant = c.variant;
         HIP_OR(launch_inverse(I, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }

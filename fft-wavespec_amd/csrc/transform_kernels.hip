@@ -118,6 +118,84 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, 2) void inverse_kernel(const dou
     }
 }
 
+// The same inverse with the C2R pre-step in registers (round 4): thread t forms the elements of its pass-0
+// layout, conj Z_k for k = (t + TPW q) + (M/R0) r, straight from X_k and X_(M-k) (two 16-B loads; each X is read
+// by two threads, the second time from L2), instead of staging all of conj Z through LDS and reading it back
+// -- one LDS round trip and one barrier fewer -- and, with SPLIT, the real/imaginary split exchanges of the
+// forward kernel (half the LDS, 3 waves per SIMD).  Z_(M/2) = conj X_(M/2) and the DC term as above.
+template <int LOG2N, int SPLIT>
+__global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_direct_kernel(
+    const double *__restrict__ in, double *__restrict__ out, const cpx<double> *__restrict__ tw, int64_t n_windows,
+    int64_t n_groups) {
+    using G = Geo<LOG2N>;
+    using T = double;
+    using v2 = V2<double>::t;
+    constexpr int N = G::N, M = G::M, TPW = G::TPW, WPB = G::WPB, SLOT = G::SLOT, B = G::B;
+    constexpr int R0 = G::R0, BPT0 = G::BPT0;
+    constexpr int ES = SPLIT ? (int)sizeof(T) : (int)sizeof(cpx<T>);
+    __shared__ __attribute__((aligned(16))) char smem[WPB * SLOT * ES];
+    const int tid = threadIdx.x;
+    const int slot = tid / TPW;
+    const int t0 = tid % TPW;
+    char *lbase = smem + slot * SLOT * ES;
+    for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+        // per window: the thread's twiddles and addresses are not hoisted out of the window loop (and spilled)
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        const int64_t w = g * WPB + slot;
+        const bool active = w < n_windows;
+        const T *xin = in + (active ? w : 0) * N;
+        cpx<T> v[16];
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q)
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const int k = (t + TPW * q) + (M / R0) * r;
+                const v2 pa = *reinterpret_cast<const v2 *>(xin + 2 * k);
+                const v2 pb = *reinterpret_cast<const v2 *>(xin + 2 * ((M - k) & (M - 1)));
+                // k = 0 only for t = 0 at (q, r) = (0, 0): real DC, X_M = 0 (branch-free selects)
+                const bool dc = (q == 0 && r == 0) && k == 0;
+                const cpx<T> xa = {pa.x, dc ? T(0) : pa.y};
+                const cpx<T> xb = {dc ? T(0) : pb.x, dc ? T(0) : pb.y};
+                const cpx<T> e = {T(0.5) * (xa.re + xb.re), T(0.5) * (xa.im - xb.im)};
+                const cpx<T> d = {T(0.5) * (xa.re - xb.re), T(0.5) * (xa.im + xb.im)};
+                const cpx<T> o = cmul(cconj(tw[k]), d);
+                const cpx<T> z = {e.re - o.im, -(e.im + o.re)};  // conj Z_k
+                v[q * R0 + r] = k == M / 2 ? cpx<T>{pa.x, pa.y} : z;  // conj(conj X_(M/2))
+                // at most 4 elements' loads in flight: hoisting all 32 sample and 16 twiddle loads spills
+                if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+        for (int q = 0; q < BPT0; ++q) dft<T, R0>(&v[q * R0]);
+        exchange<SPLIT, T, LOG2N, 0>(lbase, v, t);  // also orders the previous group's reads
+        mid_passes<SPLIT, false, T, LOG2N, 1>(lbase, v, tw, t);
+        const int bq0 = t, bq1 = t == 0 ? TPW : 2 * TPW - t;
+        cpx<T> u0[8], u1[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            u0[r] = v[r];
+            u1[r] = v[8 + r];
+        }
+        if constexpr (G::NPASS > 1) {
+            twiddle<false, T, 8>(u0, tw, 2 * bq0);
+            twiddle<false, T, 8>(u1, tw, 2 * bq1);
+        }
+        dft<T, 8>(u0);
+        dft<T, 8>(u1);
+        if (active) {
+            constexpr T kScale = T(1) / T(M);
+            T *xo = out + w * N;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                __builtin_nontemporal_store(v2{u0[r].re * kScale, -u0[r].im * kScale},
+                                            reinterpret_cast<v2 *>(xo + 2 * (bq0 + B * r)));
+                __builtin_nontemporal_store(v2{u1[r].re * kScale, -u1[r].im * kScale},
+                                            reinterpret_cast<v2 *>(xo + 2 * (bq1 + B * r)));
+            }
+        }
+    }
+}
+
 // One packed spectrum of nb bins; bins >= nb are the zeroed upper half of the
 // reference's arrays (phase 0).  256 threads, contiguous chunks, two passes:
 // correction counts -> block scan -> outputs.  Same unwrap formulation as
@@ -185,13 +263,22 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
     using namespace core;
     if (L.n_windows <= 0) return hipSuccess;
     const auto *tw = static_cast<const cpx<double> *>(L.twiddle);
+    // the C2R pre-step in registers with the split exchange at N = 2048 .. 8192 (inverse_direct_kernel); variant 1
+    // = the LDS pre-step kernel (round 1-3 form), variant 2 = the register pre-step with the AoS exchange
 #define INV_CASE(LG)                                                                                          \
     case LG: {                                                                                                \
         const int64_t groups = (L.n_windows + Geo<LG>::WPB - 1) / Geo<LG>::WPB;                               \
         int64_t grid = L.grid > 0 ? L.grid : 32768;                                                           \
         if (grid > groups) grid = groups;                                                                     \
-        hipLaunchKernelGGL(inverse_kernel<LG>, dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, L.out, tw, \
-                           L.n_windows, groups);                                                              \
+        if (L.variant == 1 || LG < 11 || LG > 13)                                                             \
+            hipLaunchKernelGGL(inverse_kernel<LG>, dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, L.out, tw, \
+                               L.n_windows, groups);                                                          \
+        else if (L.variant == 2)                                                                              \
+            hipLaunchKernelGGL((inverse_direct_kernel<LG, 0>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
+                               L.out, tw, L.n_windows, groups);                                               \
+        else                                                                                                  \
+            hipLaunchKernelGGL((inverse_direct_kernel<LG, 2>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
+                               L.out, tw, L.n_windows, groups);                                               \
         return hipGetLastError();                                                                             \
     }
     switch (L.log2n) {

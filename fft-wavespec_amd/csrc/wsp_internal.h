@@ -59,6 +59,7 @@ struct InverseLaunch {
     int64_t n_windows;
     int log2n;
     int grid;             // 0 = auto
+    int variant;          // wsp_plan_set_variant: 1 = the LDS pre-step form, 2 = register pre-step + AoS exchange
 };
 hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream);
 

@@ -312,6 +312,9 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    kernel with plain (not non-temporal) output stores;
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
+ *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
+ *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
+ *    with the AoS exchange; 0 = the pre-step in registers, split exchange;
  *  - MTB_OUT_TOPK_PHASE records (FFT kernel): 1 = the AoS form (two waves per
  *    SIMD, every thread's phase chunk) instead of the split-exchange one-wave
  *    scan + one-wave winners' phases. */

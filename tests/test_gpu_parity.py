@@ -322,6 +322,36 @@ def test_inverse_round_trip_single(gpu_session, n):
     assert np.max(np.abs(back - x)) <= 1e-13 * np.max(np.abs(x))
 
 
+@pytest.mark.parametrize("n", [1024, 2048, 4096, 8192])
+def test_inverse_forms(gpu_session, n):
+    """The inverse plan's kernel forms (wsp_plan_set_variant): 0 = the C2R pre-step in registers with the split
+    exchange (default at N = 2048 .. 8192), 1 = the pre-step through LDS (round-1 form), 2 = registers + the
+    AoS exchange: each against the oracle (1e-12 of the window's max) and within 1e-14 of each other, on a ragged
+    batch (the last workgroup's window slots past the end)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(n + 1)
+    w = 333
+    spec = rng.standard_normal((w, n))
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(spec).to(dev)
+    outs = []
+    for v in (0, 1, 2):
+        plan = bridge.Plan.inverse(0, n, w)
+        plan.set_variant(v)
+        d_o = torch.full((w * n,), float("nan"), dtype=torch.float64, device=dev)
+        plan.execute(d_in.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(d_o.view(w, n).cpu().numpy())
+        plan.close()
+    for i in range(0, w, 17):
+        want = oracle.fft_real_inverse(spec[i])
+        for o in outs:
+            assert np.max(np.abs(o[i] - want)) <= 1e-12 * np.max(np.abs(want)), i
+    scale = np.abs(outs[1]).max(axis=1, keepdims=True)
+    assert np.all(np.abs(outs[0] - outs[1]) <= 1e-14 * scale)
+    assert np.all(np.abs(outs[2] - outs[1]) <= 1e-14 * scale)
+
+
 def test_inverse_plan_full_size(gpu_session):
     """Device-resident forward (packed) -> inverse plans over 65536 x 4096 fp64 (2 GiB each way):
     round trip returns x minus its Nyquist component for every window."""
