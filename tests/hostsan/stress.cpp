@@ -10,6 +10,8 @@
 //   * device plans executed while another thread re-targets (set_topk) and
 //     destroys them;
 //   * gpu_init on another device while the session is open (must be refused);
+//   * grouped plans (wsp_group_*, the mixed-length launch and its per-length form) executed from
+//     two threads while a third toggles the mode / segment and destroys them;
 //   * pinned feeds (gpu_register_host): threads registering their series and
 //     output arrays, running synchronous batches through them, unregistering,
 //     and two threads racing to register overlapping ranges of one buffer.
@@ -44,6 +46,11 @@ struct Api {
     decltype(&wsp_plan_destroy) plan_destroy;
     decltype(&gpu_register_host) reg;
     decltype(&gpu_unregister_host) unreg;
+    decltype(&wsp_group_create) group_create;
+    decltype(&wsp_group_execute) group_execute;
+    decltype(&wsp_group_set_mode) group_set_mode;
+    decltype(&wsp_group_set_segment) group_set_segment;
+    decltype(&wsp_group_destroy) group_destroy;
 } A;
 std::atomic<int> g_fail{0};
 
@@ -156,6 +163,48 @@ void plan_race() {  // execute vs set_topk vs destroy on shared plans
         CHECK(A.plan_destroy(p) == MTB_BAD_ARGS, "double destroy");
     }
 }
+// grouped hop = 1 plans: executes racing mode / segment changes and destroy; the buffers live for the whole
+// program (the fake streams may still write them after a destroy returns)
+const int kGLens[5] = {512, 1024, 2048, 4096, 512};
+const int64_t kGWins[5] = {40, 33, 20, 7, 1};
+std::vector<std::vector<double>> g_gin, g_gout[2];
+void group_race() {
+    CHECK(A.init(0, 16) == MTB_OK, "init group");
+    for (int r = 0; r < 30; ++r) {
+        const int64_t g = A.group_create(0, 5, kGLens, kGWins, MTB_DETREND_NONE, MTB_WINDOW_HANN, MTB_PREC_F64);
+        CHECK(g > 0, "group_create");
+        std::atomic<bool> stop{false};
+        auto exec = [&](int k) {
+            const void *in[5];
+            void *out[5];
+            for (int m = 0; m < 5; ++m) {
+                in[m] = g_gin[m].data();
+                out[m] = g_gout[k][m].data();
+            }
+            while (!stop) {
+                const int st = A.group_execute(g, in, out, nullptr);
+                if (st == MTB_BAD_ARGS) break;  // destroyed
+                CHECK(st == MTB_OK, "group_execute %d", st);
+            }
+        };
+        std::thread e0(exec, 0), e1(exec, 1);
+        std::thread tg([&] {
+            for (int i = 0; i < 40 && !stop; ++i) {
+                A.group_set_mode(g, i % 2);
+                A.group_set_segment(g, i % 3 == 0 ? 0 : 7 * i);
+            }
+        });
+        std::this_thread::sleep_for(std::chrono::microseconds(300));
+        CHECK(A.group_destroy(g) == MTB_OK, "group destroy");
+        stop = true;
+        e0.join();
+        e1.join();
+        tg.join();
+        CHECK(A.group_destroy(g) == MTB_BAD_ARGS, "double group destroy");
+    }
+    A.shutdown();
+}
+
 void pinned_feed(int sym) {  // FeedCache rewired to pinned buffers, one chart's view
     CHECK(A.init(0, 16) == MTB_OK, "init pinned %d", sym);
     const int n = 128 << (sym % 3), hop = 1 + sym % 4, len = 64 * hop + n;
@@ -213,6 +262,15 @@ int main(int argc, char **argv) {
     sym(h, A.plan_destroy, "wsp_plan_destroy");
     sym(h, A.reg, "gpu_register_host");
     sym(h, A.unreg, "gpu_unregister_host");
+    sym(h, A.group_create, "wsp_group_create");
+    sym(h, A.group_execute, "wsp_group_execute");
+    sym(h, A.group_set_mode, "wsp_group_set_mode");
+    sym(h, A.group_set_segment, "wsp_group_set_segment");
+    sym(h, A.group_destroy, "wsp_group_destroy");
+    for (int m = 0; m < 5; ++m) {
+        g_gin.push_back(series_of(60 + m, (int)kGWins[m] + kGLens[m] - 1));
+        for (int k = 0; k < 2; ++k) g_gout[k].emplace_back((size_t)kGWins[m] * (kGLens[m] / 2));
+    }
 
     // the session outlives every chart below; a different device is refused while it is open
     CHECK(A.init(0, 8) == MTB_OK, "main init");
@@ -224,6 +282,7 @@ int main(int argc, char **argv) {
     th.emplace_back(plan_race);
     for (int c = 0; c < 4; ++c) th.emplace_back(pinned_feed, c);
     th.emplace_back(register_race);
+    th.emplace_back(group_race);
     for (auto &t : th) t.join();
     CHECK(early_done == 14, "early charts %d", early_done.load());
     // main's own reference still holds the session: a sync batch works
