@@ -65,6 +65,7 @@ def parse(argv=None):
                     help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
     ap.add_argument("--slide-seg", type=int, default=0, help="windows per sliding-DFT workgroup (0 = library policy)")
     ap.add_argument("--variant", type=int, default=0, help="kernel form (wsp_plan_set_variant; ablations)")
+    ap.add_argument("--chunk", type=int, default=0, help="windows per chunk of the two-pass large-N path (wsp_plan_set_chunk)")
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
                     help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
     ap.add_argument("--c5-streams", type=int, default=0,
@@ -346,7 +347,7 @@ def shard_plan(name: str, rank: int, world: int, scaling: str, c5_shard: str = "
 class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
-    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0):
+    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0, chunk=0):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -367,6 +368,8 @@ class SingleBatch(Workload):
             full = torch.randn(w * n, dtype=tdt, device=dev, generator=gen)
             self.series = full[a:b].contiguous() if (a, b) != (0, full.numel()) else full
             self.plan = bridge.Plan.inverse(local_rank, n, nw)
+            if variant:
+                self.plan.set_variant(variant)
         else:
             full = synth.random_walk_torch((w - 1) * hop + n, seed, dev, tdt)  # resident in HBM
             self.series = full[a:b].contiguous() if (a, b) != (0, full.numel()) else full
@@ -380,6 +383,8 @@ class SingleBatch(Workload):
                 self.plan.set_slide_segment(slide_seg)
             if variant:
                 self.plan.set_variant(variant)
+            if chunk:
+                self.plan.set_chunk(chunk)
         self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
         del full
         self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
@@ -569,7 +574,7 @@ def main(argv=None):
                      args.c5_streams, args.c5_mode, args.c5_shard)
     else:
         wl = SingleBatch(args.config, shard_rank, local_rank, shard_world, scaling, args.algo, args.slide_seg,
-                         args.variant)
+                         args.variant, args.chunk)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)

@@ -310,6 +310,8 @@ struct Config {
     int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
     int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
     unsigned char *scan_flags = nullptr;  // wsp_plan_set_scan_flags: per-window path of the probe-threshold top-k scan
+    int64_t chunk = 0;                  // N > 16384 two-pass path: windows per chunk, 0 = large_chunk (wsp_plan_set_chunk)
+    int64_t chunk_windows() const;
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
     int64_t record() const {
@@ -324,6 +326,8 @@ struct Config {
     int64_t series_elems() const { return (n_windows - 1) * hop + n; }
     int64_t unique_input_elems() const { return hop >= n ? n_windows * (int64_t)n : series_elems(); }
 };
+
+int64_t Config::chunk_windows() const { return chunk > 0 ? chunk : large_chunk(log2n, f32); }
 
 int ilog2_exact(int n) {
     if (n <= 0 || (n & (n - 1))) return -1;
@@ -376,7 +380,7 @@ WsLayout ws_layout(const Config &c, int dev) {
     if (c.op == kOpSpectrum && (c.detrend == MTB_DETREND_KALMAN || (large && c.detrend == MTB_DETREND_IIR)))
         det = (size_t)(c.n_windows * c.n) * es;
     if (large && c.detrend == MTB_DETREND_MEAN) means = (size_t)c.n_windows * sizeof(double);
-    if (large) y = (size_t)std::min<int64_t>(c.n_windows, large_chunk(c.log2n, c.f32)) * (size_t)(c.n / 2) * 2 * es;
+    if (large) y = (size_t)std::min<int64_t>(c.n_windows, c.chunk_windows()) * (size_t)(c.n / 2) * 2 * es;
     L.det = 0;
     L.means = align256(det);
     L.y = align256(L.means + means);
@@ -556,7 +560,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         G.means = reinterpret_cast<double *>(wsb + ws.means);
         G.y = wsb + ws.y;
         G.n_windows = c.n_windows;
-        G.chunk = large_chunk(c.log2n, c.f32);
+        G.chunk = c.chunk_windows();
         G.log2n = c.log2n;
         G.window = c.window;
         G.packed = c.output == MTB_OUT_PACKED;
@@ -1865,6 +1869,21 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
     std::lock_guard<std::mutex> lk(p->mu);
     const Config old = p->cfg;
     p->cfg.slide_seg = windows;
+    const int sw = plan_ws_fit(*p);
+    if (sw != MTB_OK) p->cfg = old;
+    return sw;
+}
+
+MTB_API int32_t wsp_plan_set_chunk(int64_t plan, int64_t windows) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || windows < 0 || windows > (int64_t(1) << 20)) {
+        set_error("wsp_plan_set_chunk(%lld, %lld): unknown plan or windows outside 0..2^20", (long long)plan,
+                  (long long)windows);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    const Config old = p->cfg;
+    p->cfg.chunk = windows;
     const int sw = plan_ws_fit(*p);
     if (sw != MTB_OK) p->cfg = old;
     return sw;

@@ -69,6 +69,7 @@ SIGNATURES = {
     "wsp_plan_set_slide_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_plan_set_variant": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_set_scan_flags": (C.c_int32, [C.c_int64, C.c_void_p]),
+    "wsp_plan_set_chunk": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -322,6 +323,10 @@ class Plan:
     def set_variant(self, variant: int) -> None:
         """Ablation: the kernel form (include/mtbridge.h wsp_plan_set_variant; 0 = the library's choice)."""
         _check("wsp_plan_set_variant", lib().wsp_plan_set_variant(self.handle, variant))
+
+    def set_chunk(self, windows: int) -> None:
+        """Tuning: windows per chunk of the two-pass large-N path (0 = the library's ~192 MiB of column results)."""
+        _check("wsp_plan_set_chunk", lib().wsp_plan_set_chunk(self.handle, windows))
 
     def set_scan_flags(self, d_flags: int) -> None:
         """Diagnostics: device buffer of n_windows bytes receiving each window's top-k scan path

@@ -326,6 +326,11 @@ MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant);
  * candidates passed the threshold than the list holds.  Other plans leave it
  * untouched.  The records are the same either way. */
 MTB_API int32_t wsp_plan_set_scan_flags(int64_t plan, void *d_flags);
+/* Tuning: windows per chunk of the two-pass large-N path (N > 16384: column
+ * results of one chunk of windows are written and read back per launch pair),
+ * 0 = the library's ~192 MiB of column results; grows the plan workspace as
+ * needed.  MTB_BAD_ARGS for an unknown plan or windows outside 0..2^20. */
+MTB_API int32_t wsp_plan_set_chunk(int64_t plan, int64_t windows);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
 

@@ -89,6 +89,29 @@ def test_large_chunks(gpu_session):
     assert oracle.rel_err(p, ref(s, n, 2048, "iir", "hann", 1024)) <= TOL["f64"]
 
 
+@pytest.mark.parametrize("n,chunk", [(262144, 5), (131072, 1), (32768, 100)])
+def test_large_set_chunk(gpu_session, n, chunk):
+    """wsp_plan_set_chunk: the two-pass path over other chunk lengths (ragged last chunk, one window per chunk)
+    gives the same records as the library's chunking (the same kernels on other chunk boundaries)."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    nwin = 13 if n > 65536 else 211
+    s = synth.random_walk(nwin * n, seed=n // 4096 + chunk)
+    d_s = torch.from_numpy(s).to(dev)
+    outs = []
+    for c in (0, chunk):
+        plan = bridge.Plan(0, n, n, nwin, "mean", "hann")
+        plan.set_variant(1)  # the two-pass path
+        plan.set_chunk(c)
+        o = torch.empty(nwin * plan.record, dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(o.cpu().numpy().reshape(nwin, plan.record))
+        plan.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert oracle.rel_err(outs[1][:2], ref(s[:2 * n], n, n, "mean", "hann", 0)) <= TOL["f64"]
+
+
 def test_large_fft_real_forward(gpu_session):
     """gpu_fft_real_forward at the legacy default InpFFTWindow = 65536."""
     n = 65536
