@@ -455,8 +455,8 @@ def test_topk_phase(gpu_session, n, hop, k, minp, maxp):
 def test_topk_phase_split_form(gpu_session, n, k, minp, maxp, window):
     """MTB_OUT_TOPK_PHASE without detrend at N = 2048 / 4096 (ns_topk_phase's instantiation): the split-exchange
     form (one-wave scan, then one wave for the winners' phases: geometric unwrap decisions, atan2 only at each
-    winner and its neighbours) against the AoS form (wsp_plan_set_variant 1: every thread's phase chunk) --
-    identical records, the same decisions and the same fma -- and against the oracle.  Bands whose bins
+    winner and its neighbours) against the AoS form (wsp_plan_set_variant 1: every thread's phase chunk) -- the
+    same bins and powers to 1e-12 -- and both against the oracle (phases and delays to 1e-8).  Bands whose bins
     0 .. kmax + 1 take 2 / 4 / 8 / 16 bins per lane, and one beyond the split slot (periods 3-300: the AoS form)."""
     torch = pytest.importorskip("torch")
     nwin = 300
@@ -473,19 +473,26 @@ def test_topk_phase_split_form(gpu_session, n, k, minp, maxp, window):
         torch.cuda.synchronize()
         outs.append(d_o.view(nwin, k, 6).cpu().numpy())
         plan.close()
-    assert np.array_equal(outs[0], outs[1])
+    # the same scan order and unwrap decisions; not bit-identical, because the AoS form evaluates the cosine windows
+    # by rotation and the split form by the three-term recurrence (9e-16 of the window)
+    a, b = outs
+    same = a[:, :, 0] == b[:, :, 0]
+    assert int((~same).sum()) <= 2
+    den = np.abs(b[:, :, 1]).max(axis=1, keepdims=True)
+    assert np.all(np.abs(np.where(same, a[:, :, 1] - b[:, :, 1], 0.0)) <= 1e-12 * den)
     got = outs[0]
     want = oracle.batch_topk_phase(s, n, n, "none", window, 0, None, k, minp, maxp)
     _topk_match(got[:, :, :4], want[:, :, :4], 1e-10, ref(s, n, n, "none", window).max(axis=1))
     full = oracle.batch_phase(s, n, n, "none", window)
-    for w in range(nwin):
-        mag = np.sqrt(full[w, 0])
-        ok = mag >= 1e-9 * mag.max()
-        same = (got[w, :, 0] == want[w, :, 0]) & (want[w, :, 0] >= 0)
-        b = want[w, same, 0].astype(int)
-        if ok[: max(b.max(initial=0), 1) + 2].all():
-            assert np.max(np.abs(got[w, same, 4:] - want[w, same, 4:]), initial=0.0) <= 1e-8
-        assert np.all(got[w, want[w, :, 0] < 0, 4:] == 0.0)
+    for g in outs:
+        for w in range(nwin):
+            mag = np.sqrt(full[w, 0])
+            ok = mag >= 1e-9 * mag.max()
+            same = (g[w, :, 0] == want[w, :, 0]) & (want[w, :, 0] >= 0)
+            bins = want[w, same, 0].astype(int)
+            if ok[: max(bins.max(initial=0), 1) + 2].all():
+                assert np.max(np.abs(g[w, same, 4:] - want[w, same, 4:]), initial=0.0) <= 1e-8
+            assert np.all(g[w, want[w, :, 0] < 0, 4:] == 0.0)
 
 
 @pytest.mark.parametrize("length", [2, 6, 64, 1000, 4096, 10002])
