@@ -742,9 +742,11 @@ __device__ __forceinline__ int unwrap_corr(cpx<double> A, cpx<double> B) {
 // neighbours (lane s: slot s, `bin` its bin or -1): u = phi + 2 pi K (the same fma), delay -(u[b+1] - u[b-1]) / 2
 // (bin 0: -(u[1] - u[0])), clamped to +-100 (L/WaveSpecZZ_1.0.4-new.mq5:1102-1119).  64 CH >= kmax + 2.
 template <int CH>
-__device__ __forceinline__ void topk_phase_wave(const cpx<double> *xrow, int M, int kmax, int k, int lane, int bin, double *rec,
-                                                bool active) {
+__device__ __forceinline__ void topk_phase_wave(const cpx<double> *xrow, int M, int kmax, int k, int lane_in, int bin,
+                                                double *rec, bool active) {
     constexpr double k2Pi = 2.0 * 3.14159265358979323846;
+    int lane = lane_in;
+    asm volatile("" : "+v"(lane));  // per window: the lane's addresses are not hoisted out of the window loop
     static_assert(CH <= 16, "two 32-bit correction masks per lane");
     const int top = kmax + 1;  // highest bin any winner's unwrapped phase or delay reads
     auto X = [&](int kk) { return kk < M && kk <= top ? xrow[kk] : cpx<double>{0.0, 0.0}; };
@@ -1127,6 +1129,10 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         T *prow = reinterpret_cast<T *>(lbase);  // power row staged in this window's LDS slot
         constexpr bool kDirect = OUT == kOutPower && (VAR & kVarDirectStore);
         if constexpr (OUT != kOutPacked && !kDirect) __syncthreads();  // every final-pass LDS read is done
+        // bin indices of the R2C slots; for the split top-k + phase form recomputed per window (pinned), so that the
+        // 16 staging addresses and bound tests are not hoisted out of the window loop and spilled
+        int tb0 = t;
+        if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(tb0));
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const cpx<T> A = u0[s], Bv = u1[7 - s];
@@ -1136,8 +1142,8 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             const cpx<T> wo = cmul(wk, o);
             cpx<T> xa = cadd(e, wo);                   // 2 X[k_A]
             cpx<T> xb = {e.re - wo.re, wo.im - e.im};  // 2 X[M - k_A]
-            int ka = t + B * s, kb = M - ka;
-            if (t == 0) {
+            int ka = tb0 + B * s, kb = M - ka;
+            if (tb0 == 0) {
                 ka = s < 4 ? B / 2 + B * s : B * (s - 4);
                 kb = s == 4 ? M / 2 : M - ka;
                 if (s == 4) {  // self-paired bins: X[0] real, X[M/2] = conj Z[M/2]
