@@ -853,7 +853,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
 
     const int tid = threadIdx.x;
     const int slot = tid / TPW;
-    const int t = tid % TPW;
+    int t = tid % TPW;  // re-pinned per window in the split top-k + phase form (below)
     char *lbase = smem + slot * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));  // this window's LDS slot
 
     // per-thread window rotation start: th_i at i = 2 (t + TPW q)
@@ -877,6 +877,9 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     if (kPrefetch && g < g_end) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
 
     for (; g < g_end; g += g_step) {
+        // split top-k + phase: every address and twiddle that depends on t is recomputed per window instead of being
+        // hoisted out of the window loop -- the 168-VGPR budget of 3 waves per SIMD has no room for them
+        if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(t));
         const int64_t w = g * WPB + slot;
         const bool active = w < a.n_windows;
         if (!kPrefetch) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
