@@ -299,14 +299,21 @@ def test_slide_topk_exact_ties(gpu_session, case):
         assert np.array_equal(outs[0], outs[v]), v
     want = oracle.batch_topk(s, n, 1, detrend, "hann", 0, None, k, 18.0, 200.0)
     kmin, kmax = oracle.band(n)
-    tied = np.all(want[:, :, 1] == 0.0, axis=1)  # windows whose band is exactly zero
+    x = s - (1.0 if detrend == "mean" else 0.0)
+    tied = np.array([not np.any(x[w:w + n]) for w in range(nwin)])  # windows of exactly zero (detrended) samples
     assert tied.sum() > 0
     first_k = np.arange(kmin, kmin + k, dtype=np.float64)
     assert np.all(want[tied, :, 0] == first_k)
     assert np.all(outs[0][tied, :, 0] == first_k) and np.all(outs[0][tied, :, 1] == 0.0)
-    if (~tied).any():
-        spec = oracle.batch_spectrum(s, n, 1, detrend, "hann")
-        _topk_bars(outs[0][~tied], want[~tied], spec[~tied, kmin:kmax + 1].max(axis=1), max_swaps=4)
+    spec = oracle.batch_spectrum(s, n, 1, detrend, "hann")
+    band_max = spec[:, kmin:kmax + 1].max(axis=1)
+    # the first window that sees the walk holds it only in its last sample, which the symmetric Hann window weighs
+    # by exactly 0 in the oracle; the sliding DFT's cosine-sum decomposition leaves rounding there (~1e-35)
+    edge = ~tied & (band_max == 0.0)
+    assert np.all(outs[0][edge, :, 1] <= 1e-30)
+    rest = ~tied & ~edge
+    if rest.any():
+        _topk_bars(outs[0][rest], want[rest], band_max[rest], max_swaps=4)
 
 
 def test_slide_topk_vs_fft_c4(gpu_session):
