@@ -64,10 +64,13 @@ for step in "$@"; do
         cfg=${val%%,*}
         extra=""
         [ "$cfg" != "$val" ] && extra=${val#*,}
-        run 300 $O/bench_$cfg.json $O/bench_$cfg.err python bench.py --config $cfg --steps 100 --warmup 20 --no-cpu-baseline ${extra//,/ }
+        # one file per (config, arguments): repeated A/B steps do not overwrite each other
+        tagx=$(echo "${extra//,/_}" | tr -c 'A-Za-z0-9_.\n-' '_')
+        bf=$O/bench_$cfg${tagx:+_$tagx}
+        run 300 $bf.json $bf.err python bench.py --config $cfg --steps 100 --warmup 20 --no-cpu-baseline ${extra//,/ }
         python3 -c "
-import json; d=json.loads(open('$O/bench_$cfg.json').read().strip().splitlines()[-1])
-print('$cfg', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g win/s'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+import json; d=json.loads(open('$bf.json').read().strip().splitlines()[-1])
+print('$cfg', '$extra', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g win/s'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
         ;;
     default)
         run 400 $O/bench_default.json $O/bench_default.err python bench.py
