@@ -1164,6 +1164,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     for (int i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
+    m.bsmall = g.mode == 2 ? 2 : 4;
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1184,7 +1185,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     auto close_class = [&]() {
         if (nc < 0) return;
         const int l2 = m.log2n[nc];
-        const int P = kMixNT * 2 * (l2 <= 10 ? 2 : 4) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
+        const int P = kMixNT * 2 * (l2 <= 10 ? m.bsmall : 4) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
         m.nseg[nc] = (int)segs;
         m.task0[nc] = (int)tasks;
         tasks += (segs + P - 1) / P;
@@ -1994,7 +1995,7 @@ MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, vo
         }
     std::lock_guard<std::mutex> lk(g->mu);
     const hipStream_t caller = (hipStream_t)hip_stream;
-    if (g->mix_ok && g->mode == 0) {
+    if (g->mix_ok && g->mode != 1) {
         HIP_OR(hipSetDevice(g->dev), MTB_BACKEND_UNAVAILABLE);
         return group_execute_mixed(*g, d_series, d_out, caller);
     }
@@ -2076,13 +2077,13 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
     std::shared_ptr<Group> g = find_group(group);
     if (!g) return -1;
     std::lock_guard<std::mutex> lk(g->mu);
-    return g->mix_ok && g->mode == 0 ? 1 : (int32_t)g->launch.size();
+    return g->mix_ok && g->mode != 1 ? 1 : (int32_t)g->launch.size();
 }
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 1) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..1", (long long)group, mode);
+    if (!g || mode < 0 || mode > 2) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..2", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

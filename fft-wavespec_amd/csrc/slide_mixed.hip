@@ -99,9 +99,11 @@ __device__ __forceinline__ bool mix_seg(MixP m, int c, int64_t s, const void *&s
     return true;
 }
 
-template <typename T, int LOG2N, int NF, int DETREND>
+template <typename T, int LOG2N, int NF, int DETREND, int BS>
 __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq) {
-    constexpr int N = 1 << LOG2N, M = N / 2, B = slide_b<LOG2N>(), NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
+    // BS: bins per thread for N <= 1024 (4 by default: the short windows' tasks then hold 4 / 8 segments side by
+    // side, as many bins per thread-step as the long ones; 2 = the per-length launches' geometry, ablation)
+    constexpr int N = 1 << LOG2N, M = N / 2, B = LOG2N <= 10 ? BS : 4, NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
                   NM = (NF - 1) / 2;
     constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
     static_assert(P * N <= 4096 && CH * REC / 2 <= N && P * NT == kMixNT, "sub-workgroup geometry");
@@ -209,7 +211,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     __syncthreads();  // the staged uniforms' reads before the next task's writes
 }
 
-template <typename T, int NF, int DETREND>
+template <typename T, int NF, int DETREND, int BS>
 __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     const MixP m = (MixP)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ d2 lds[4096];
@@ -234,10 +236,10 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
             if (c == i) t0 = m->task0[i], l2 = m->log2n[i];
         const int64_t local = task - t0;
         switch (l2) {
-        case 12: mix_task<T, 12, NF, DETREND>(m, c, local, lds, twq); break;
-        case 11: mix_task<T, 11, NF, DETREND>(m, c, local, lds, twq); break;
-        case 10: mix_task<T, 10, NF, DETREND>(m, c, local, lds, twq); break;
-        default: mix_task<T, 9, NF, DETREND>(m, c, local, lds, twq); break;
+        case 12: mix_task<T, 12, NF, DETREND, BS>(m, c, local, lds, twq); break;
+        case 11: mix_task<T, 11, NF, DETREND, BS>(m, c, local, lds, twq); break;
+        case 10: mix_task<T, 10, NF, DETREND, BS>(m, c, local, lds, twq); break;
+        default: mix_task<T, 9, NF, DETREND, BS>(m, c, local, lds, twq); break;
         }
     }
     if (tid == 0) {  // the last workgroup out resets this execute's counter slot
@@ -253,7 +255,8 @@ template <typename T, int NF, int DETREND> int resident_t(int dev) {
     static std::atomic<int> per_cu{0};
     int pc = per_cu.load(std::memory_order_relaxed);
     if (pc == 0) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND>, kMixNT, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND, 4>, kMixNT, 0) !=
+                hipSuccess ||
             pc <= 0)
             pc = 1;
         per_cu.store(pc, std::memory_order_relaxed);
@@ -269,9 +272,9 @@ template <typename T> int resident_nf(int nf, int detrend, int dev) {
     return mean ? resident_t<T, 3, kDetrendMean>(dev) : resident_t<T, 3, kDetrendNone>(dev);
 }
 
-template <typename T> hipError_t launch_nf(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
+template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
     const bool mean = detrend == kDetrendMean;
-#define MIX(NF_, D_) hipLaunchKernelGGL((slide_mixed_kernel<T, NF_, D_>), dim3((unsigned)grid), dim3(kMixNT), 0, s, m)
+#define MIX(NF_, D_) hipLaunchKernelGGL((slide_mixed_kernel<T, NF_, D_, BS>), dim3((unsigned)grid), dim3(kMixNT), 0, s, m)
     if (nf == 1) {
         if (mean) MIX(1, kDetrendMean);
         else MIX(1, kDetrendNone);
@@ -291,11 +294,12 @@ int slide_mix_resident(int nf, int detrend, bool f32, int dev) {
 
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t s) {
     if ((nf != 1 && nf != 3) || grid < 1 || m.nclass < 1 || m.nclass > kMixClass || m.n_tasks < 1 || !m.counter ||
-        !m.done || !m.tw4096)
+        !m.done || !m.tw4096 || (m.bsmall != 2 && m.bsmall != 4))
         return hipErrorInvalidValue;
     for (int c = 0; c < m.nclass; ++c)
         if (m.log2n[c] < 9 || m.log2n[c] > 12 || m.seg[c] < 1 || !m.omega[c]) return hipErrorInvalidValue;
-    return f32 ? launch_nf<float>(m, nf, detrend, grid, s) : launch_nf<double>(m, nf, detrend, grid, s);
+    if (m.bsmall == 2) return f32 ? launch_nf<float, 2>(m, nf, detrend, grid, s) : launch_nf<double, 2>(m, nf, detrend, grid, s);
+    return f32 ? launch_nf<float, 4>(m, nf, detrend, grid, s) : launch_nf<double, 4>(m, nf, detrend, grid, s);
 }
 
 }  // namespace wsp

@@ -829,6 +829,38 @@ __device__ __forceinline__ void load_group(const SpecArgs<T> &a, int64_t g, int 
     }
 }
 
+// The same loads through a buffer descriptor based at the window (split top-k + phase form): one 32-bit lane offset
+// and 16 scalar offsets instead of 16 64-bit addresses (32 VGPRs), which that form's 168-VGPR budget needs; the
+// 16-B loads are element-aligned for odd hops (unaligned mode), so there is no two-scalar path either.
+template <typename T, int LOG2N, int AUX>
+__device__ __forceinline__ void load_group_buf_aux(__amdgpu_buffer_rsrc_t rs, int t, typename V2<T>::t (&raw)[16]) {
+    using G = Geo<LOG2N>;
+    using v2 = typename V2<T>::t;
+#pragma unroll
+    for (int q = 0; q < G::BPT0; ++q)
+#pragma unroll
+        for (int r = 0; r < G::R0; ++r) {
+            const int voff = 2 * (t + G::TPW * q) * (int)sizeof(T), soff = 2 * (G::M / G::R0) * r * (int)sizeof(T);
+            if constexpr (sizeof(T) == 8)
+                raw[q * G::R0 + r] = __builtin_bit_cast(v2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX));
+            else
+                raw[q * G::R0 + r] = __builtin_bit_cast(v2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, AUX));
+        }
+}
+// (a wave never straddles two windows here: TPW >= 64, so the window base is wave-uniform -- readfirstlane puts
+// the descriptor in SGPRs)
+template <typename T, int LOG2N>
+__device__ __forceinline__ void load_group_buf(const SpecArgs<T> &a, int64_t w, int t, typename V2<T>::t (&raw)[16]) {
+    using G = Geo<LOG2N>;
+    static_assert(G::TPW >= 64, "one window per wave");
+    const uint64_t base = reinterpret_cast<uint64_t>(a.series + (w < a.n_windows ? w : 0) * a.hop);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    T *xw = reinterpret_cast<T *>(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(xw, (short)0, (int)(G::N * sizeof(T)), 0x00020000);
+    if (a.nt) load_group_buf_aux<T, LOG2N, 2>(rs, t, raw);  // nt: streamed once when windows do not overlap
+    else load_group_buf_aux<T, LOG2N, 0>(rs, t, raw);
+}
+
 template <typename T, int LOG2N, int DETREND, int OUT, int WCLASS, int VAR>
 __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((VAR & kVarOcc4) ? 4 : 3) : 2) void spectrum_kernel(SpecArgs<T> a) {
     using G = Geo<LOG2N>;
@@ -848,7 +880,12 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     constexpr int kScan = 16 * 8 + ((OUT == kOutTopK || OUT == kOutTopKPhase) && TPW >= 128 ? NWV * 64 * (8 + 4) : 0) +
                           (OUT == kOutTopKPhase ? WPB * (M < 64 ? M : 64) * 4 : 0);
     static_assert(!kPhase || sizeof(T) == 8, "phase outputs are fp64");
-    __shared__ __attribute__((aligned(16))) char smem[kMain + kScan];
+    // split top-k + phase: the per-thread window rotation start lives in LDS and the window constants are re-read
+    // from the kernarg segment per window, so none of them holds a VGPR across the window loop (168-VGPR budget)
+    constexpr bool kCosWin = WCLASS == kWinCos || WCLASS == kWinCos2;
+    constexpr bool kPinWin = OUT == kOutTopKPhase && kSplit;
+    constexpr int kStash = kPinWin && kCosWin ? 2 * BPT0 * TPW * 8 : 0;
+    __shared__ __attribute__((aligned(16))) char smem[kMain + kScan + kStash];
     double *scanbuf = reinterpret_cast<double *>(smem + kMain);
 
     const int tid = threadIdx.x;
@@ -857,11 +894,20 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     char *lbase = smem + slot * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));  // this window's LDS slot
 
     // per-thread window rotation start: th_i at i = 2 (t + TPW q)
-    constexpr bool kCosWin = WCLASS == kWinCos || WCLASS == kWinCos2;
     double wc0[BPT0], ws0[BPT0];
     if constexpr (kCosWin) {
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) sincos(a.inv_theta * (double)(2 * (t + TPW * q)), &ws0[q], &wc0[q]);
+    }
+    double *stash = reinterpret_cast<double *>(smem + kMain + kScan);
+    if constexpr (kStash > 0) {
+        if (slot == 0)
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q) {
+                stash[q * TPW + t] = wc0[q];
+                stash[(BPT0 + q) * TPW + t] = ws0[q];
+            }
+        __syncthreads();
     }
 
     // group sequence of this workgroup: cyclic (g = b + i*grid, the default:
@@ -882,12 +928,22 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(t));
         const int64_t w = g * WPB + slot;
         const bool active = w < a.n_windows;
-        if (!kPrefetch) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
         double xa[16], xb[16];
+        if constexpr (OUT == kOutTopKPhase && kSplit) {
+            v2 rw[16];  // this window's samples only: nothing carried across windows
+            load_group_buf<T, LOG2N>(a, w, t, rw);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            xa[i] = (double)raw[i].x;
-            xb[i] = (double)raw[i].y;
+            for (int i = 0; i < 16; ++i) {
+                xa[i] = (double)rw[i].x;
+                xb[i] = (double)rw[i].y;
+            }
+        } else {
+            if (!kPrefetch) load_group<T, LOG2N, VAR>(a, g, slot, t, raw);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                xa[i] = (double)raw[i].x;
+                xb[i] = (double)raw[i].y;
+            }
         }
         if (kPrefetch && g + g_step < g_end) load_group<T, LOG2N, VAR>(a, g + g_step, slot, t, raw);
 
@@ -984,6 +1040,18 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
 
         // ---- window (fp64) + pass 0 (no twiddles: Ns = 1)
         cpx<T> v[16];
+        double A0 = a.a0, A1 = a.a1, A2 = a.a2, CS = a.cs, SS = a.ss, CO = a.co, SO = a.so;
+        if constexpr (kPinWin && kCosWin) {
+            typedef const __attribute__((address_space(4))) SpecArgs<T> *KP;
+            KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(kp));  // one scalar load per window instead of 12 VGPRs held across the loop
+            A0 = kp->a0, A1 = kp->a1, A2 = kp->a2, CS = kp->cs, SS = kp->ss, CO = kp->co, SO = kp->so;
+#pragma unroll
+            for (int q = 0; q < BPT0; ++q) {
+                wc0[q] = stash[q * TPW + t];
+                ws0[q] = stash[(BPT0 + q) * TPW + t];
+            }
+        }
         constexpr bool kRec = (VAR & kVarWinRec) && WCLASS == kWinCos && R0 >= 8;
         if constexpr ((VAR & kVarWinTab) && kCosWin) {
 #pragma unroll
@@ -998,14 +1066,14 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             // odd samples i0 + 1 + D r: h_(r+1) = 2C h_r - h_(r-1) + a0 (2 - 2C), C = cos(th D) = a.cs.
             // Seeds h_0, h_1 of both sequences from the per-thread rotation start; the recurrence
             // amplifies rounding by at most 1/sin(th D) (~2.6 at R0 = 16) over <= 15 steps.
-            const double C2 = 2.0 * a.cs, K = a.a0 * (2.0 - C2);
+            const double C2 = 2.0 * CS, K = A0 * (2.0 - C2);
 #pragma unroll
             for (int q = 0; q < BPT0; ++q) {
                 double c = wc0[q], s = ws0[q];
                 asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no hoisted seeds
-                const double c1 = c * a.cs - s * a.ss, s1 = s * a.cs + c * a.ss;
-                double he0 = a.a0 + a.a1 * c, he1 = a.a0 + a.a1 * c1;
-                double ho0 = a.a0 + a.a1 * (c * a.co - s * a.so), ho1 = a.a0 + a.a1 * (c1 * a.co - s1 * a.so);
+                const double c1 = c * CS - s * SS, s1 = s * CS + c * SS;
+                double he0 = A0 + A1 * c, he1 = A0 + A1 * c1;
+                double ho0 = A0 + A1 * (c * CO - s * SO), ho1 = A0 + A1 * (c1 * CO - s1 * SO);
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
                     v[q * R0 + r] = {T(xa[q * R0 + r] * he0), T(xb[q * R0 + r] * ho0)};
@@ -1029,16 +1097,16 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             for (int r = 0; r < R0; ++r) {
                 double da = xa[q * R0 + r], db = xb[q * R0 + r];
                 if constexpr (kCosWin) {
-                    const double co = c * a.co - s * a.so;  // th_(i+1)
+                    const double co = c * CO - s * SO;  // th_(i+1)
                     if constexpr (WCLASS == kWinCos2) {      // Blackman: + a2 cos 2th
-                        da *= a.a0 + a.a1 * c + a.a2 * (2.0 * c * c - 1.0);
-                        db *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
+                        da *= A0 + A1 * c + A2 * (2.0 * c * c - 1.0);
+                        db *= A0 + A1 * co + A2 * (2.0 * co * co - 1.0);
                     } else {                                 // Hann 0.5(1 - cos), Hamming
-                        da *= a.a0 + a.a1 * c;
-                        db *= a.a0 + a.a1 * co;
+                        da *= A0 + A1 * c;
+                        db *= A0 + A1 * co;
                     }
-                    const double cn = c * a.cs - s * a.ss;
-                    s = s * a.cs + c * a.ss;
+                    const double cn = c * CS - s * SS;
+                    s = s * CS + c * SS;
                     c = cn;
                 } else if constexpr (WCLASS == kWinBartlett) {
                     int tq = t + TPW * q;

@@ -151,15 +151,17 @@ struct SlideGroup {
 hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream_t stream);
 // Mixed-length grouped launch (slide_mixed.hip): the members of a group of window lengths 512 .. 4096 in ONE
 // persistent launch.  A 512-thread workgroup takes tasks from a device counter; a task is one segment of a
-// 4096-pt member, or 512 / NT(N) segments of a shorter length side by side (2 x 2048, 2 x 1024, 4 x 512: one
-// sub-workgroup of NT = N / (2 B) threads each).  Tasks run longest windows first, so the four lengths' seed
-// phases and drains overlap instead of each launch paying its own.  Members are laid out class by class
+// 4096-pt member, or 512 / NT(N) segments of a shorter length side by side (one sub-workgroup of NT = N / (2 B)
+// threads each).  Tasks run longest windows first, so the four lengths' seed
+// phases and drains overlap instead of each launch paying its own (with 4 bins per thread at every length, a task
+// is 1 / 2 / 4 / 8 segments at N = 4096 / 2048 / 1024 / 512).  Members are laid out class by class
 // (class c = one window length, longest first); series / out are the caller's pointers of this execute.
 constexpr int kMixMax = 32;    // members per mixed launch
 constexpr int kMixClass = 4;   // window lengths 4096, 2048, 1024, 512
 constexpr int kMixNT = 512;    // threads per workgroup
 struct SlideMix {
     int nclass, n_tasks;
+    int bsmall;                         // bins per thread for N <= 1024: 4 (default) or 2; N >= 2048 always 4
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];

@@ -14,9 +14,9 @@ from pathlib import Path
 
 out, cfg = Path(sys.argv[1]), sys.argv[2]
 key = sys.argv[3] if len(sys.argv) > 3 else cfg  # e.g. c4_fft: the config under a forced algorithm
-OURS = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "slide_seed_kernel", "slide_seed_r_kernel", "fused_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "col_kernel", "row_kernel", "mean_kernel",
+OURS = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "slide_seed_kernel", "slide_seed_r_kernel", "fused_kernel", "kalman_detrend_kernel", "kalman_pk2_kernel", "kalman_pk4_kernel", "inverse_kernel", "inverse_direct_kernel", "col_kernel", "row_kernel", "mean_kernel",
         "iir_kernel")
-MAIN = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "inverse_kernel", "row_kernel",
+MAIN = ("spectrum_kernel", "slide_kernel", "slide_mixed_kernel", "slide_topk_kernel", "slide_topk_t_kernel", "slide_topk_p_kernel", "inverse_kernel", "inverse_direct_kernel", "row_kernel",
         "fused_kernel")  # one per step; a Kalman pre-pass adds to its step
 
 
