@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU-issue roofline of the VALU-bound configurations from rocprofv3 SQ counter passes.
 
-    python scripts/valu_roofline.py [<cfg>=<sq csv> ...]   (default: the committed profiles/r03/sq passes)
+    python scripts/valu_roofline.py [<cfg>=<sq csv> ...]   (default: the committed profiles/r04/sq passes)
 
 Writes profiles/valu.json, which bench.py reads into `roofline.valu` for those configurations (their
 `roofline.bound` is then "valu"; the HBM fraction stays beside it).  Per kernel and dispatch:
@@ -24,7 +24,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-DEFAULT = {"c3": "profiles/r03/sq/c3_sq_counters.csv", "c4_topk": "profiles/r03/sq/c4_topk_sq_counters.csv"}
+DEFAULT = {"c3": "profiles/r04/sq/c3_sq_counters.csv", "c4_topk": "profiles/r04/sq/c4_topk_sq_counters.csv"}
 SIMDS, SES = 1024, 32
 
 
