@@ -1157,24 +1157,26 @@ constexpr int kMixSlots = 256;  // counter slots: executes of one group in fligh
 
 // One persistent launch over every member (slide_mixed.hip), on the caller's stream.  Members are laid out class by
 // class, longest windows first; segment length S over the whole batch: about two tasks per resident workgroup (a task
-// = S windows x 2048 bins, half that for N <= 1024), 32..256 windows (wsp_group_set_segment overrides it).
+// = S windows x 2048 bins, half that for N <= 1024), 128..256 windows (wsp_group_set_segment overrides it).  The
+// floor of 128: a segment's seed (a full FFT) costs tens of slides, and at small batches (a one-eighth C5 shard)
+// shorter segments lost more to seeds than they gained in balance (0.142 ms at 32 against 0.122 at 128, r04d).
 int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_out, hipStream_t s) {
     const int n = (int)g.cfg.size();
     std::vector<int> order(n);
     for (int i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
-    m.bsmall = g.mode == 2 ? 2 : 4;
+    m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
-    const int res = slide_mix_resident(nf, det, c0.f32, g.dev);
+    const int res = slide_mix_resident(nf, det, c0.f32, m.bsmall, g.dev);
     int64_t bins = 0;
     for (const Config &c : g.cfg) bins += c.n_windows * (int64_t)(c.n / 2);
     int64_t S = g.seg;
     if (S <= 0) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
-        S = std::min<int64_t>(256, std::max<int64_t>(32, S));
+        S = std::min<int64_t>(256, std::max<int64_t>(128, S));
     }
     Tables t4096;
     int st = get_tables(g.dev, 12, false, &t4096);

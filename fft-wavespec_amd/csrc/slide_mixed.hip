@@ -251,11 +251,11 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     }
 }
 
-template <typename T, int NF, int DETREND> int resident_t(int dev) {
+template <typename T, int NF, int DETREND, int BS> int resident_t(int dev) {
     static std::atomic<int> per_cu{0};
     int pc = per_cu.load(std::memory_order_relaxed);
     if (pc == 0) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND, 4>, kMixNT, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND, BS>, kMixNT, 0) !=
                 hipSuccess ||
             pc <= 0)
             pc = 1;
@@ -266,10 +266,10 @@ template <typename T, int NF, int DETREND> int resident_t(int dev) {
     return pc * cus;
 }
 
-template <typename T> int resident_nf(int nf, int detrend, int dev) {
+template <typename T, int BS> int resident_nf(int nf, int detrend, int dev) {
     const bool mean = detrend == kDetrendMean;
-    if (nf == 1) return mean ? resident_t<T, 1, kDetrendMean>(dev) : resident_t<T, 1, kDetrendNone>(dev);
-    return mean ? resident_t<T, 3, kDetrendMean>(dev) : resident_t<T, 3, kDetrendNone>(dev);
+    if (nf == 1) return mean ? resident_t<T, 1, kDetrendMean, BS>(dev) : resident_t<T, 1, kDetrendNone, BS>(dev);
+    return mean ? resident_t<T, 3, kDetrendMean, BS>(dev) : resident_t<T, 3, kDetrendNone, BS>(dev);
 }
 
 template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
@@ -288,8 +288,9 @@ template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, in
 
 }  // namespace
 
-int slide_mix_resident(int nf, int detrend, bool f32, int dev) {
-    return f32 ? resident_nf<float>(nf, detrend, dev) : resident_nf<double>(nf, detrend, dev);
+int slide_mix_resident(int nf, int detrend, bool f32, int bsmall, int dev) {
+    if (bsmall == 2) return f32 ? resident_nf<float, 2>(nf, detrend, dev) : resident_nf<double, 2>(nf, detrend, dev);
+    return f32 ? resident_nf<float, 4>(nf, detrend, dev) : resident_nf<double, 4>(nf, detrend, dev);
 }
 
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t s) {

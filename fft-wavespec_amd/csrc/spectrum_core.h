@@ -641,6 +641,12 @@ __device__ __forceinline__ void topk_rounds(int t, int kmin, int span, int k, XF
     }
 }
 
+// atan2 as a call (the top-k + phase forms): inlined into the window loop, its ~19 fp64 polynomial coefficients are
+// materialised in VGPRs once and hoisted out of the loop (38 VGPRs held across the FFT: 20-212 B/lane of spills in
+// those forms); as a call they are rebuilt inside it, per call.  The full phase record (kOutPhase: 18 atan2 per
+// lane, unspilled at N = 4096) keeps them inline for the interleaving of its independent atan2 chains.
+__device__ __noinline__ double atan2_call(double y, double x) { return atan2(y, x); }
+
 // Phase, unwrap and group delay of one window (CalculateFFTPhase, UnwrapPhase,
 // CalculateGroupDelay: L/WaveSpecZZ_1.0.4-new.mq5:1040-1120, called at :3225-3227
 // with n = N over the GPU unpack of :3183-3196, i.e. X_k for k < N/2 and zeros
@@ -650,7 +656,7 @@ __device__ __forceinline__ void topk_rounds(int t, int kmin, int span, int k, XF
 // equals phi_i + 2 pi K_i with K_i the running count of +-1 corrections: K is
 // an exact integer prefix scan and u is one fma, so only the rounding of the
 // reference's running sum (not its decisions) differs.
-template <int LOG2N, int CH = 16>
+template <int LOG2N, int CH = 16, bool kCall = false>
 __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, double *scanbuf, double (&pw)[CH],
                                             double (&u)[CH], double (&gd)[CH]) {
     // CH = bins per thread (16: the whole row; smaller for the top-k records, which only need the
@@ -667,7 +673,7 @@ __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, doub
         ph[j] = 0.0;  // bin M: the zeroed upper half, atan2(0, 0) = 0
         if (k >= 0 && k < M) {
             const cpx<double> x = xrow[pad16(k)];
-            ph[j] = atan2(x.im, x.re);
+            ph[j] = kCall ? atan2_call(x.im, x.re) : atan2(x.im, x.re);
             if (j >= 1 && j <= CH) pw[j - 1] = x.re * x.re + x.im * x.im;
         }
     }
@@ -772,22 +778,34 @@ __device__ __forceinline__ void topk_phase_wave(const cpx<double> *xrow, int M, 
         if (lane >= d) incl += up;
     }
     const int K = incl - sum;  // corrections of every bin < k0
-    const int b = bin >= 0 ? bin : 0;
+    // the 3k unwrapped phases u[b_s - 1], u[b_s], u[b_s + 1] of the k winners as items l = 3 s + i spread over the
+    // lanes (one atan2 per lane and pass: a single pass for k <= 21), then gathered back to lane s
     double um = 0.0, u0 = 0.0, up = 0.0;
+    const int passes = (3 * k + 63) / 64;
 #pragma unroll 1
-    for (int i = 0; i < 3; ++i) {  // u[b - 1], u[b], u[b + 1] (one atan2 in the code); every lane takes part
-        const int bb = b - 1 + i < 0 ? 0 : b - 1 + i;
+    for (int p = 0; p < passes; ++p) {
+        const int l = 64 * p + lane, s = l / 3 < 64 ? l / 3 : 63, i = l - 3 * (l / 3);
+        const int bs = __shfl(bin, s, 64);
+        const int bb = (bs >= 0 ? bs : 0) - 1 + i < 0 ? 0 : (bs >= 0 ? bs : 0) - 1 + i;
         const int ob = bb / CH < 64 ? bb / CH : 63, jb = bb - CH * ob;
         const int Ko = __shfl(K, ob, 64);
         const unsigned po = (unsigned)__shfl((int)pos, ob, 64), no = (unsigned)__shfl((int)neg, ob, 64);
         const unsigned m = jb >= 31 ? 0xffffffffu : (2u << jb) - 1u;
         const int Kb = Ko + __popc(po & m) - __popc(no & m);
         const cpx<double> x = X(bb);
-        const double uu = fma((double)Kb, k2Pi, bb < M ? atan2(x.im, x.re) : 0.0);
-        um = i == 0 ? uu : um;
-        u0 = i == 1 ? uu : u0;
-        up = i == 2 ? uu : up;
+        const double uu = fma((double)Kb, k2Pi, bb < M ? atan2_call(x.im, x.re) : 0.0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int src = 3 * lane + j;  // this lane's winner's item j
+            const double v = __shfl(uu, src & 63, 64);
+            if ((src >> 6) == p) {
+                um = j == 0 ? v : um;
+                u0 = j == 1 ? v : u0;
+                up = j == 2 ? v : up;
+            }
+        }
     }
+    const int b = bin >= 0 ? bin : 0;
     const double u3[3] = {um, u0, up};
     double g = b == 0 ? -(u3[2] - u3[1]) : -(u3[2] - u3[0]) / 2.0;
     if (g > 100.0) g = 100.0;
@@ -880,12 +898,8 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     constexpr int kScan = 16 * 8 + ((OUT == kOutTopK || OUT == kOutTopKPhase) && TPW >= 128 ? NWV * 64 * (8 + 4) : 0) +
                           (OUT == kOutTopKPhase ? WPB * (M < 64 ? M : 64) * 4 : 0);
     static_assert(!kPhase || sizeof(T) == 8, "phase outputs are fp64");
-    // split top-k + phase: the per-thread window rotation start lives in LDS and the window constants are re-read
-    // from the kernarg segment per window, so none of them holds a VGPR across the window loop (168-VGPR budget)
     constexpr bool kCosWin = WCLASS == kWinCos || WCLASS == kWinCos2;
-    constexpr bool kPinWin = OUT == kOutTopKPhase && kSplit;
-    constexpr int kStash = kPinWin && kCosWin ? 2 * BPT0 * TPW * 8 : 0;
-    __shared__ __attribute__((aligned(16))) char smem[kMain + kScan + kStash];
+    __shared__ __attribute__((aligned(16))) char smem[kMain + kScan];
     double *scanbuf = reinterpret_cast<double *>(smem + kMain);
 
     const int tid = threadIdx.x;
@@ -898,16 +912,6 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     if constexpr (kCosWin) {
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) sincos(a.inv_theta * (double)(2 * (t + TPW * q)), &ws0[q], &wc0[q]);
-    }
-    double *stash = reinterpret_cast<double *>(smem + kMain + kScan);
-    if constexpr (kStash > 0) {
-        if (slot == 0)
-#pragma unroll
-            for (int q = 0; q < BPT0; ++q) {
-                stash[q * TPW + t] = wc0[q];
-                stash[(BPT0 + q) * TPW + t] = ws0[q];
-            }
-        __syncthreads();
     }
 
     // group sequence of this workgroup: cyclic (g = b + i*grid, the default:
@@ -1040,18 +1044,6 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
 
         // ---- window (fp64) + pass 0 (no twiddles: Ns = 1)
         cpx<T> v[16];
-        double A0 = a.a0, A1 = a.a1, A2 = a.a2, CS = a.cs, SS = a.ss, CO = a.co, SO = a.so;
-        if constexpr (kPinWin && kCosWin) {
-            typedef const __attribute__((address_space(4))) SpecArgs<T> *KP;
-            KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-            asm volatile("" : "+s"(kp));  // one scalar load per window instead of 12 VGPRs held across the loop
-            A0 = kp->a0, A1 = kp->a1, A2 = kp->a2, CS = kp->cs, SS = kp->ss, CO = kp->co, SO = kp->so;
-#pragma unroll
-            for (int q = 0; q < BPT0; ++q) {
-                wc0[q] = stash[q * TPW + t];
-                ws0[q] = stash[(BPT0 + q) * TPW + t];
-            }
-        }
         constexpr bool kRec = (VAR & kVarWinRec) && WCLASS == kWinCos && R0 >= 8;
         if constexpr ((VAR & kVarWinTab) && kCosWin) {
 #pragma unroll
@@ -1066,14 +1058,14 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             // odd samples i0 + 1 + D r: h_(r+1) = 2C h_r - h_(r-1) + a0 (2 - 2C), C = cos(th D) = a.cs.
             // Seeds h_0, h_1 of both sequences from the per-thread rotation start; the recurrence
             // amplifies rounding by at most 1/sin(th D) (~2.6 at R0 = 16) over <= 15 steps.
-            const double C2 = 2.0 * CS, K = A0 * (2.0 - C2);
+            const double C2 = 2.0 * a.cs, K = a.a0 * (2.0 - C2);
 #pragma unroll
             for (int q = 0; q < BPT0; ++q) {
                 double c = wc0[q], s = ws0[q];
                 asm volatile("" : "+v"(c), "+v"(s));  // recompute per window: no hoisted seeds
-                const double c1 = c * CS - s * SS, s1 = s * CS + c * SS;
-                double he0 = A0 + A1 * c, he1 = A0 + A1 * c1;
-                double ho0 = A0 + A1 * (c * CO - s * SO), ho1 = A0 + A1 * (c1 * CO - s1 * SO);
+                const double c1 = c * a.cs - s * a.ss, s1 = s * a.cs + c * a.ss;
+                double he0 = a.a0 + a.a1 * c, he1 = a.a0 + a.a1 * c1;
+                double ho0 = a.a0 + a.a1 * (c * a.co - s * a.so), ho1 = a.a0 + a.a1 * (c1 * a.co - s1 * a.so);
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
                     v[q * R0 + r] = {T(xa[q * R0 + r] * he0), T(xb[q * R0 + r] * ho0)};
@@ -1097,16 +1089,16 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
             for (int r = 0; r < R0; ++r) {
                 double da = xa[q * R0 + r], db = xb[q * R0 + r];
                 if constexpr (kCosWin) {
-                    const double co = c * CO - s * SO;  // th_(i+1)
+                    const double co = c * a.co - s * a.so;  // th_(i+1)
                     if constexpr (WCLASS == kWinCos2) {      // Blackman: + a2 cos 2th
-                        da *= A0 + A1 * c + A2 * (2.0 * c * c - 1.0);
-                        db *= A0 + A1 * co + A2 * (2.0 * co * co - 1.0);
+                        da *= a.a0 + a.a1 * c + a.a2 * (2.0 * c * c - 1.0);
+                        db *= a.a0 + a.a1 * co + a.a2 * (2.0 * co * co - 1.0);
                     } else {                                 // Hann 0.5(1 - cos), Hamming
-                        da *= A0 + A1 * c;
-                        db *= A0 + A1 * co;
+                        da *= a.a0 + a.a1 * c;
+                        db *= a.a0 + a.a1 * co;
                     }
-                    const double cn = c * CS - s * SS;
-                    s = s * CS + c * SS;
+                    const double cn = c * a.cs - s * a.ss;
+                    s = s * a.cs + c * a.ss;
                     c = cn;
                 } else if constexpr (WCLASS == kWinBartlett) {
                     int tq = t + TPW * q;
@@ -1194,16 +1186,17 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         // the 1/2 of E, O (and 1/4 of |X|^2): folded into the window coefficients for the cosine
         // windows (make_args halves a0, a1, a2 -- an exact power-of-two scaling, bit-identical results)
         constexpr T kS1 = kCosWin ? T(1) : T(0.5), kS2 = kCosWin ? T(1) : T(0.25);
-        const cpx<T> wt = a.tw[t];
-        const cpx<T> wlo = t == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
-        const cpx<T> whi = t == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
         T *prow = reinterpret_cast<T *>(lbase);  // power row staged in this window's LDS slot
         constexpr bool kDirect = OUT == kOutPower && (VAR & kVarDirectStore);
         if constexpr (OUT != kOutPacked && !kDirect) __syncthreads();  // every final-pass LDS read is done
-        // bin indices of the R2C slots; for the split top-k + phase form recomputed per window (pinned), so that the
-        // 16 staging addresses and bound tests are not hoisted out of the window loop and spilled
+        // bin indices and twiddle of the R2C slots; for the split top-k + phase form recomputed here (pinned after the
+        // barrier), so that neither the twiddle load nor the 16 staging addresses and bound tests are issued at the
+        // top of the window and held (spilled) across its FFT
         int tb0 = t;
         if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(tb0));
+        const cpx<T> wt = a.tw[tb0];
+        const cpx<T> wlo = tb0 == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
+        const cpx<T> whi = tb0 == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const cpx<T> A = u0[s], Bv = u1[7 - s];
@@ -1432,7 +1425,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 auto add_phase = [&](auto chv) {
                     constexpr int CH = decltype(chv)::value;
                     double pwc[CH], uc[CH], gdc[CH];
-                    phase_chunk<LOG2N, CH>(reinterpret_cast<const cpx<double> *>(lbase), t, scanbuf, pwc, uc, gdc);
+                    phase_chunk<LOG2N, CH, true>(reinterpret_cast<const cpx<double> *>(lbase), t, scanbuf, pwc, uc, gdc);
                     const int nk = a.topk < KW ? a.topk : KW;
                     for (int s2 = 0; s2 < nk; ++s2) {
                         const int b = win[s2];

@@ -161,7 +161,7 @@ constexpr int kMixClass = 4;   // window lengths 4096, 2048, 1024, 512
 constexpr int kMixNT = 512;    // threads per workgroup
 struct SlideMix {
     int nclass, n_tasks;
-    int bsmall;                         // bins per thread for N <= 1024: 4 (default) or 2; N >= 2048 always 4
+    int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];
@@ -177,7 +177,7 @@ struct SlideMix {
 // One launch of `grid` persistent workgroups (grid <= the resident count, slide_mix_resident).
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t stream);
 // Resident 512-thread workgroups of the mixed kernel on device `dev` (occupancy x CUs).
-int slide_mix_resident(int nf, int detrend, bool f32, int dev);
+int slide_mix_resident(int nf, int detrend, bool f32, int bsmall, int dev);
 
 // hop = 1 top-k records ([bin, power, Re, Im] x topk per window, MTB_OUT_TOPK) by the sliding DFT: the
 // band's trackers only (span <= 512), one wave per segment, the FFT kernel's one-wave scan per window.

@@ -337,7 +337,7 @@ hipError_t launch_slide_group(const SlideArgs &a, const SlideGroup &g, hipStream
     });
     return hipSuccess;
 }
-int slide_mix_resident(int, int, bool, int) { return 512; }
+int slide_mix_resident(int, int, bool, int, int) { return 512; }
 hipError_t launch_slide_mix(const SlideMix &m, int, int, bool f32, int grid, hipStream_t s) {  // every member, same records
     if (grid < 1 || m.nclass < 1 || m.n_tasks < 1 || !m.counter || !m.done) return hipErrorInvalidValue;
     int64_t total = 0;
