@@ -1167,6 +1167,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
     m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
+    m.nt = g.mode == 3;
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -2084,8 +2085,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 2) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..2", (long long)group, mode);
+    if (!g || mode < 0 || mode > 3) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..3", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

@@ -138,6 +138,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     const d2 *__restrict__ hwin = omega + NF * M;
     const d2 *__restrict__ mod = omega + (NF + 1) * M;  // [NM][N] e^{-j m th i}
     const double lvl = (DETREND == kDetrendMean && on) ? (double)x[0] : 0.0;
+    const bool nt = m->nt;  // uniform
 
     // ---- seeds: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}) (seed_ffts), trackers of this thread's bins
     d2 om[B][NF], tr[B][NF];
@@ -202,7 +203,9 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
 #pragma unroll
             for (int q = 0; q < B / 2; ++q) {
                 typedef T v2t __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
+                const v2t v = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
+                if (nt) __builtin_nontemporal_store(v, reinterpret_cast<v2t *>(out + 2 * NT * q));
+                else *reinterpret_cast<v2t *>(out + 2 * NT * q) = v;
             }
             out += M;
             if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);

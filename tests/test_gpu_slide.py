@@ -460,7 +460,7 @@ def test_stateful_plan_on_two_streams(gpu_session, kind):
     plan.close()
 
 
-@pytest.mark.parametrize("mode", ["auto", "per-length", "mixed-b4"])
+@pytest.mark.parametrize("mode", ["auto", "per-length", "mixed-b4", "mixed-nt"])
 @pytest.mark.parametrize("prec,detrend,window", [("f64", "none", "hann"), ("f64", "mean", "blackman"),
                                                  ("f32", "mean", "hamming"), ("f64", "none", "none")])
 def test_group_mixed_members(gpu_session, prec, detrend, window, mode):
@@ -478,7 +478,7 @@ def test_group_mixed_members(gpu_session, prec, detrend, window, mode):
     outs = [torch.empty(nw * (n // 2), dtype=tdt, device=dev) for n, nw in zip(lens, nwins)]
     g = bridge.Group(0, lens, nwins, detrend, window, prec)
     g.set_mode(mode)
-    mixed = mode in ("auto", "mixed-b4") and window != "blackman"
+    mixed = mode != "per-length" and window != "blackman"
     assert g.launches == (1 if mixed else 2 + 3)  # per length: 512's 19 members in two launches; 1024, 2048, 4096
     g.execute([x.data_ptr() for x in series], [o.data_ptr() for o in outs], torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
