@@ -65,17 +65,17 @@ struct ColArgs {
     double a0, a1, a2, cd, sd, c1, s1, inv_theta, inv_nm1;  // window: rotation by th*2*M1*TP per r, th per odd sample
 };
 
-constexpr int kCB = 16;  // columns per workgroup in col_kernel
+constexpr int kCB = 16;  // columns per workgroup in col_kernel (CB: 8 for fp64 M2 = 512, see col_cb)
 
-template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN>
-__global__ __launch_bounds__(kCB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) {
+template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, int CB = kCB>
+__global__ __launch_bounds__(CB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) {
     using G = LGeo<LOG2M2>;
-    constexpr int M1 = 1 << LOG2M1, M2 = G::L, TP = G::TP, NB1 = M1 / kCB;
+    constexpr int M1 = 1 << LOG2M1, M2 = G::L, TP = G::TP, NB1 = M1 / CB;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    __shared__ cpx<T> lds[kCB * G::SLOT];
-    const int tid = threadIdx.x, c = tid % kCB, t = tid / kCB;
+    __shared__ cpx<T> lds[CB * G::SLOT];
+    const int tid = threadIdx.x, c = tid % CB, t = tid / CB;
     const int beta = blockIdx.x % NB1;
-    const int n1 = beta * kCB + c;
+    const int n1 = beta * CB + c;
     const T *__restrict__ series = static_cast<const T *>(a.series);
     const cpx<T> *__restrict__ tw = static_cast<const cpx<T> *>(a.tw);
     cpx<T> *__restrict__ y = static_cast<cpx<T> *>(a.y);
@@ -98,8 +98,8 @@ __global__ __launch_bounds__(kCB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a)
             }
         }
     };
-    // register prefetch of the next window (64 VGPRs in fp64) except at M2 = 512, whose
-    // 512-thread workgroup has only 256 VGPRs per lane
+    // register prefetch of the next window (64 VGPRs in fp64) except at fp64 M2 = 512, whose FFT leaves no room
+    // for it within 256 VGPRs (the 8-column form overlaps loads and FFTs by running two workgroups per CU instead)
     constexpr bool kPrefetch = LOG2M2 < 9 || sizeof(T) == 4;
     const int64_t wstep = gridDim.x / NB1;
     int64_t wc = blockIdx.x / NB1;
@@ -562,13 +562,23 @@ int64_t windows_in_flight(int64_t nwin, int blocks_per_window, size_t lds_bytes)
     return std::max<int64_t>(1, std::min<int64_t>(nwin, slots / blocks_per_window));
 }
 
-template <typename T, int LM1, int LM2, int WC, bool MEAN>
-hipError_t col_launch(const large::ColArgs &a, hipStream_t s) {
-    constexpr int NB1 = (1 << LM1) / large::kCB;
-    const int64_t g = windows_in_flight(a.nwin, NB1, large::kCB * large::LGeo<LM2>::SLOT * sizeof(core::cpx<T>)) * NB1;
-    hipLaunchKernelGGL((large::col_kernel<T, LM1, LM2, WC, MEAN>), dim3((unsigned)g), dim3(large::kCB * (1 << LM2) / 16), 0,
+template <typename T, int LM1, int LM2, int WC, bool MEAN, int CB = large::kCB>
+hipError_t col_launch_cb(const large::ColArgs &a, hipStream_t s) {
+    constexpr int NB1 = (1 << LM1) / CB;
+    const int64_t g = windows_in_flight(a.nwin, NB1, CB * large::LGeo<LM2>::SLOT * sizeof(core::cpx<T>)) * NB1;
+    hipLaunchKernelGGL((large::col_kernel<T, LM1, LM2, WC, MEAN, CB>), dim3((unsigned)g), dim3(CB * (1 << LM2) / 16), 0,
                        s, a);
     return hipGetLastError();
+}
+
+// fp64 M2 = 512 (N = 262144): 8 columns per workgroup by default -- 256 threads and 70 KiB of LDS, so two
+// independent workgroups per CU whose loads, FFTs and stores overlap, against one 512-thread workgroup per CU
+// (16 columns, 139 KiB: loads, FFT and stores back to back); variant 6 keeps the 16-column form (A/B)
+template <typename T, int LM1, int LM2, int WC, bool MEAN>
+hipError_t col_launch(const large::ColArgs &a, int variant, hipStream_t s) {
+    if constexpr (LM2 == 9 && sizeof(T) == 8)
+        if (variant != 6) return col_launch_cb<T, LM1, LM2, WC, MEAN, 8>(a, s);
+    return col_launch_cb<T, LM1, LM2, WC, MEAN>(a, s);
 }
 
 template <typename T, int LM1, int LM2, bool PACKED> hipError_t row_launch(const large::RowArgs &a, hipStream_t s) {
@@ -584,7 +594,7 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
     hipError_t e;
     using namespace core;
 #define COL(WC)                                                                            \
-    e = mean ? col_launch<T, LM1, LM2, WC, true>(ca, s) : col_launch<T, LM1, LM2, WC, false>(ca, s)
+    e = mean ? col_launch<T, LM1, LM2, WC, true>(ca, L.variant, s) : col_launch<T, LM1, LM2, WC, false>(ca, L.variant, s)
     switch (wclass) {
     case kWinCos: COL(kWinCos); break;
     case kWinCos2: COL(kWinCos2); break;

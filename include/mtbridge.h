@@ -298,7 +298,7 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
-/* Tuning / ablation: the kernel form, 0..5 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..6 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -309,7 +309,8 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    windows; 2 = the same pipelined over two internal streams; 3 = the fused
  *    one-workgroup-per-window kernel (N = 65536 / 131072; the default for fp64
  *    N = 65536); 4 = its 256-thread form with register prefetch; 5 = the fused
- *    kernel with plain (not non-temporal) output stores;
+ *    kernel with plain (not non-temporal) output stores; 6 = fp64 N = 262144
+ *    with 16-column column-pass workgroups (the default takes 8);
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
