@@ -170,7 +170,7 @@ template <int LOG2M1> struct RowGeo {
     static constexpr int RB = LOG2M1 >= 8 ? 8 : 16;  // rows (and mirror rows) per workgroup
 };
 
-template <typename T, int LOG2M1, int LOG2M2, bool PACKED>
+template <typename T, int LOG2M1, int LOG2M2, bool PACKED, bool XCD = true>
 __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void row_kernel(RowArgs a) {
     using G = LGeo<LOG2M1>;
     constexpr int RB = RowGeo<LOG2M1>::RB;
@@ -178,7 +178,12 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
     constexpr int64_t M = (int64_t)M1 * M2;
     __shared__ cpx<T> lds[2 * RB * G::SLOT];
     const int tid = threadIdx.x, rho = tid / TP, t = tid % TP;
-    const int beta = blockIdx.x % NB2;
+    // XCD-aware block order: blocks b and b + 8 share an XCD (round-robin dealing, MI355X_MICROARCH.md), so
+    // virtual block (b % 8) * (grid / 8) + b / 8 puts row blocks beta and beta + 1 -- each writes runs of RB
+    // consecutive bins, the two halves of the same output lines at RB = 8 in fp64 -- on one XCD's L2
+    const int vb = XCD && gridDim.x % 8 == 0 ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8)
+                                             : (int)blockIdx.x;
+    const int beta = vb % NB2;
     // slot rho < RB: row beta*RB + rho; slot RB + i: row M2 - (beta*RB + i), or M2/2 for i = 0 of block 0
     auto row_of = [&](int s) {
         const int i = s < RB ? s : s - RB, lo = beta * RB + i;
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
     const int N = 1 << a.log2n;
     cpx<T> *slot = lds + rho * G::SLOT;
     const int64_t wstep = gridDim.x / NB2;
-    int64_t wc = blockIdx.x / NB2;
+    int64_t wc = vb / NB2;
     cpx<T> nxt[16];
     auto load = [&](int64_t w) {
         const cpx<T> *__restrict__ yr = static_cast<const cpx<T> *>(a.y) + (w * M2 + row) * (int64_t)M1;
@@ -581,10 +586,15 @@ hipError_t col_launch(const large::ColArgs &a, int variant, hipStream_t s) {
     return col_launch_cb<T, LM1, LM2, WC, MEAN>(a, s);
 }
 
-template <typename T, int LM1, int LM2, bool PACKED> hipError_t row_launch(const large::RowArgs &a, hipStream_t s) {
+// variant 7: the row pass in plain block order (A/B of the XCD-aware order)
+template <typename T, int LM1, int LM2, bool PACKED>
+hipError_t row_launch(const large::RowArgs &a, int variant, hipStream_t s) {
     constexpr int RB = large::RowGeo<LM1>::RB, NB2 = ((1 << LM2) / 2) / RB;
     const int64_t g = windows_in_flight(a.nwin, NB2, 2 * RB * large::LGeo<LM1>::SLOT * sizeof(core::cpx<T>)) * NB2;
-    hipLaunchKernelGGL((large::row_kernel<T, LM1, LM2, PACKED>), dim3((unsigned)g), dim3(2 * RB * (1 << LM1) / 16), 0, s, a);
+    if (variant == 7)
+        hipLaunchKernelGGL((large::row_kernel<T, LM1, LM2, PACKED, false>), dim3((unsigned)g), dim3(2 * RB * (1 << LM1) / 16), 0, s, a);
+    else
+        hipLaunchKernelGGL((large::row_kernel<T, LM1, LM2, PACKED>), dim3((unsigned)g), dim3(2 * RB * (1 << LM1) / 16), 0, s, a);
     return hipGetLastError();
 }
 
@@ -603,7 +613,7 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
     }
 #undef COL
     if (e != hipSuccess) return e;
-    return L.packed ? row_launch<T, LM1, LM2, true>(ra, s) : row_launch<T, LM1, LM2, false>(ra, s);
+    return L.packed ? row_launch<T, LM1, LM2, true>(ra, L.variant, s) : row_launch<T, LM1, LM2, false>(ra, L.variant, s);
 }
 
 // the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablations: variant 3 =
