@@ -1,0 +1,13 @@
+# round-4 session check g: the mixed C5 launch per window length (one-length groups: which class runs below the
+# write rate), two vs four bins per thread there, and the segment length of the slowest one-eighth C5 shards
+# (rank 1 = the N = 1024 symbols, rank 4 = N = 4096).
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+S1=--emulate-shard,1/8
+S4=--emulate-shard,4/8
+bash scripts/gpu_run.sh r04g harness=c5_len_sweep.py,30,0,128,256 harness=c5_len_sweep.py,30,0,128,--mode,mixed-b4 \
+    harness=c5_len_sweep.py,30,0,--mode,per-length \
+    bench=c5,$S1 bench=c5,$S1,--slide-seg,64 bench=c5,$S1,--slide-seg,96 bench=c5,$S1,--slide-seg,192 \
+    bench=c5,$S1,--c5-mode,group-mixed-b4 bench=c5,$S4 bench=c5,$S4,--slide-seg,64 bench=c5,$S4,--slide-seg,192 \
+    bench=c5,$S4,--c5-mode,group-mixed-b4 bench=large
