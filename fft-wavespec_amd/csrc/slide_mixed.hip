@@ -138,7 +138,6 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     const d2 *__restrict__ hwin = omega + NF * M;
     const d2 *__restrict__ mod = omega + (NF + 1) * M;  // [NM][N] e^{-j m th i}
     const double lvl = (DETREND == kDetrendMean && on) ? (double)x[0] : 0.0;
-    const bool nt = m->nt;  // uniform
 
     // ---- seeds: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}) (seed_ffts), trackers of this thread's bins
     d2 om[B][NF], tr[B][NF];
@@ -203,9 +202,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
 #pragma unroll
             for (int q = 0; q < B / 2; ++q) {
                 typedef T v2t __attribute__((ext_vector_type(2)));
-                const v2t v = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
-                if (nt) __builtin_nontemporal_store(v, reinterpret_cast<v2t *>(out + 2 * NT * q));
-                else *reinterpret_cast<v2t *>(out + 2 * NT * q) = v;
+                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
             }
             out += M;
             if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
@@ -224,7 +221,20 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     for (int i = tid; i < 1024; i += kMixNT) twq[i] = tw[i];
     int *ldsi = reinterpret_cast<int *>(lds);
     for (;;) {
-        if (tid == 0) ldsi[0] = atomicAdd(m->counter, 1);
+        if (tid == 0) {
+            if (m->two_ended) {
+                // ablation (wsp_group_set_mode 3): every other group of 8 workgroups takes tasks from the end
+                // (shortest windows first), so concurrently running workgroups are at different phases (seed or
+                // slide) instead of all seeding at once; front + back < n_tasks decides on one 64-bit counter
+                const bool back = (blockIdx.x >> 3) & 1;
+                const unsigned long long old =
+                    atomicAdd(reinterpret_cast<unsigned long long *>(m->counter), back ? (1ull << 32) : 1ull);
+                const int f = (int)(old & 0xffffffffull), bk = (int)(old >> 32);
+                ldsi[0] = f + bk >= m->n_tasks ? m->n_tasks : (back ? m->n_tasks - 1 - bk : f);
+            } else {
+                ldsi[0] = atomicAdd(m->counter, 1);
+            }
+        }
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(ldsi[0]);  // uniform: the task's scalars stay in SGPRs
         __syncthreads();
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     if (tid == 0) {  // the last workgroup out resets this execute's counter slot
         __threadfence();
         if (atomicAdd(m->done, 1) == (int)gridDim.x - 1) {
-            atomicExch(m->counter, 0);
+            atomicExch(reinterpret_cast<unsigned long long *>(m->counter), 0ull);  // both words of either order
             atomicExch(m->done, 0);
         }
     }

@@ -164,14 +164,15 @@ constexpr int kMixNT = 512;    // threads per workgroup
 struct SlideMix {
     int nclass, n_tasks;
     int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
-    int nt;                             // power rows stored non-temporally (wsp_group_set_mode 3)
+    int two_ended;                      // half the workgroups take tasks from the end (wsp_group_set_mode 3)
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];
     double s0, s1, s2;                  // a0, a1/2, a2/2 of the (common) window
     const void *omega[kMixClass];       // slide table of class c (SlideArgs::omega)
     const void *tw4096;                 // W_4096^k, double complex: the quarter table of every length
-    int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup)
+    int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup;
+                                        // counter 8-B aligned: 64-bit [front | back << 32] in the two-ended order)
     int64_t sg0[kMixMax];               // member i: its first segment within its class
     int64_t n_windows[kMixMax];
     const void *series[kMixMax];

@@ -386,8 +386,9 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * counter, longest windows first); otherwise one launch per window length.
  * 1 = one launch per window length (lanes: wsp_group_set_streams); 2 = the
  * mixed launch with four bins per thread at every length (ablation; the
- * default takes two for N <= 1024); 3 = the mixed launch with non-temporal
- * stores of the power rows (ablation).  MTB_BAD_ARGS outside 0..3. */
+ * default takes two for N <= 1024); 3 = the mixed launch with every other
+ * group of 8 workgroups taking tasks from the end of the list (ablation).
+ * MTB_BAD_ARGS outside 0..3. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
