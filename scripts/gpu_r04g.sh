@@ -2,7 +2,7 @@
 # write rate), two vs four bins per thread there, and the segment length of the slowest one-eighth C5 shards
 # (rank 1 = the N = 1024 symbols, rank 4 = N = 4096); first the two-ended task order (mode 3: every other group
 # of 8 workgroups takes the shortest tasks first, so seed phases stop coinciding) against the default; last the
-# fused N = 65536 kernel with wave-local column FFTs (variant 8) against the default.
+# fused N = 65536 kernel with wave-local column FFTs (variant 8) and wave-local rows too (9) against the default.
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -19,4 +19,4 @@ bash scripts/gpu_run.sh r04g bench=c5 bench=c5,--c5-mode,group-mixed-two-ended b
     bench=c5,$S1 bench=c5,$S1,--slide-seg,64 bench=c5,$S1,--slide-seg,96 bench=c5,$S1,--slide-seg,192 \
     bench=c5,$S1,--c5-mode,group-mixed-b4 bench=c5,$S4 bench=c5,$S4,--slide-seg,64 bench=c5,$S4,--slide-seg,192 \
     bench=c5,$S4,--c5-mode,group-mixed-b4 bench=large bench=large,--variant,8 bench=large,--steps,101 \
-    bench=large,--variant,8,--steps,101
+    bench=large,--variant,8,--steps,101 bench=large,--variant,9 bench=large,--variant,9,--steps,101
