@@ -277,17 +277,8 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
-//
-// WLR (wave-local rows): a wave holds SPW / 2 rows and their SPW / 2 mirror rows (SPW = 64 / TPR slots per wave),
-// so the row FFT's exchanges and the R2C step's partner read need only the wave fence; the output staging, which
-// spans every slot's LDS, keeps the workgroup barriers.
-// WL (wave-local columns): each column's TPC threads are lanes of one wave (64 / TPC columns per wave, lane =
-// column-in-wave + (64 / TPC) * transform thread) instead of one lane per column across the workgroup, so the
-// column FFTs exchange through LDS with a wave fence instead of a workgroup barrier and the waves walk the
-// column blocks independently -- one wave's loads overlap another's FFT and stores; row segments are read as
-// (64 / TPC) x 16 B pieces (64 B at M2 = 256: each 128-B line is read by two neighbouring waves).
 template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true,
-          bool NTS = false, bool WL = false, bool WLR = false>
+          bool NTS = false>
 __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
@@ -308,16 +299,9 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     const int N = 1 << a.log2n;
     using v2 = typename core::V2<T>::t;
     // column pass geometry (col_kernel): column c of the block, transform thread t
-    static_assert(!WL || (64 % TPC == 0 && !PF), "wave-local columns: whole transforms per wave, no prefetch");
-    constexpr int CPW = 64 / TPC;  // WL: columns per wave
-    const int cc = WL ? (tid / 64) * CPW + (tid % 64) % CPW : tid % CB;
-    const int ct = WL ? (tid % 64) / CPW : tid / CB;
+    const int cc = tid % CB, ct = tid / CB;
     // row pass geometry (row_kernel): slot rho, transform thread t
-    static_assert(!WLR || (64 % (2 * TPR) == 0 && RB == (NT / 64) * (64 / TPR / 2)), "wave-local rows: slot pairs per wave");
-    constexpr int HB = 64 / TPR / 2;  // WLR: rows (and as many mirror rows) per wave
-    const int rgrp = (tid % 64) / TPR, rwav = tid / 64;
-    const int rho = WLR ? (rgrp < HB ? rwav * HB + rgrp : RB + rwav * HB + (rgrp - HB)) : tid / TPR;
-    const int rt = tid % TPR;
+    const int rho = tid / TPR, rt = tid % TPR;
     v2 raw[16];
     auto load_cols = [&](int64_t w, int beta) {  // 16 sample pairs of column beta * CB + cc
         const T *__restrict__ xw = series + w * a.hop;
@@ -393,7 +377,7 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
             }
             // next block's samples in flight during this FFT (not across the row pass: registers)
             if (PF && beta + 1 < NB1) load_cols(w, beta + 1);
-            wg_fft<T, LOG2M2, 1, WL>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
+            wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
             constexpr int R = last_radix<LOG2M2>();
             const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
 #pragma unroll
@@ -419,13 +403,13 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = nxt[r];
             if (PF && beta2 + 1 < NB2) load_rows(beta2 + 1);
-            wg_fft<T, LOG2M1, 1, WLR>(v, slot, rt, tw, a.log2n);
+            wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
             constexpr int R = last_radix<LOG2M1>();
 #pragma unroll
             for (int q = 0; q < 16 / R; ++q)
 #pragma unroll
                 for (int r = 0; r < R; ++r) slot[pad16(rt + TPR * q + (M1 / R) * r)] = v[q * R + r];
-            wg::fft_sync<WLR>();  // the partner slot is this wave's (WLR) or any wave's
+            __syncthreads();
             const bool self = row == 0 || row == M2 / 2;
             const cpx<T> *pslot = lds + (self ? rho : (rho < RB ? rho + RB : rho - RB)) * GR::SLOT;
             T res[16][PACKED ? 2 : 1];
@@ -634,7 +618,7 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
 
 // the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablations: variant 3 =
 // 512 threads without register prefetch, two waves per SIMD; variant 4 = 256 threads with prefetch)
-template <typename T, int LM1, int NT, bool PF, bool NTS = false, bool WL = false, bool WLR = false>
+template <typename T, int LM1, int NT, bool PF, bool NTS = false>
 hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const large::RowArgs &ra, int wclass, bool mean,
                         hipStream_t s) {
     large::ColArgs ca = ca0;
@@ -647,11 +631,11 @@ hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const l
     using namespace core;
 #define FUSED(WC)                                                                                                          \
     if (mean) {                                                                                                            \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS, WL, WLR>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF, NTS, WL, WLR>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     } else {                                                                                                               \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF, NTS, WL, WLR>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF, NTS, WL, WLR>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     }
     switch (wclass) {
     case kWinCos: FUSED(kWinCos); break;
@@ -782,12 +766,6 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
                            : fused_launch<T, 8, 512, false, true>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 5 && log2m == 15)  // ablation: the fused form with plain output stores
         return fused_launch<T, 7, 512, false, false>(L, ca, ra, wclass, means != nullptr, s);
-    if (L.variant == 8 && (log2m == 15 || log2m == 16))  // the fused form with wave-local column FFTs
-        return log2m == 15 ? fused_launch<T, 7, 512, false, true, true>(L, ca, ra, wclass, means != nullptr, s)
-                           : fused_launch<T, 8, 512, false, true, true>(L, ca, ra, wclass, means != nullptr, s);
-    if (L.variant == 9 && (log2m == 15 || log2m == 16))  // ... and wave-local row FFTs + R2C pairs
-        return log2m == 15 ? fused_launch<T, 7, 512, false, true, true, true>(L, ca, ra, wclass, means != nullptr, s)
-                           : fused_launch<T, 8, 512, false, true, true, true>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 4 && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7, 256, true>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8, 256, true>(L, ca, ra, wclass, means != nullptr, s);

@@ -1119,7 +1119,7 @@ struct Group {
     // and there are at most kMixMax members; wsp_group_set_mode(1) forces the per-length launches
     bool mix_ok = false;
     int mode = 0;
-    int *ctr = nullptr;                    // 256 task-counter slots (64-bit counter, done, pad) on the device, zeroed at create
+    int *ctr = nullptr;                    // 256 task-counter slots (counter, done) on the device, zeroed at create
     uint32_t exec_no = 0;
     // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
     std::vector<hipStream_t> streams;
@@ -1166,8 +1166,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     for (int i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
-    m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
-    m.two_ended = g.mode == 3;
+    m.bsmall = g.mode == 2 ? 4 : g.mode == 3 ? 1 : 2;  // mix_bins; N = 1024 at 2: 0.737 ms against 0.777 (4), r04d
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1188,7 +1187,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     auto close_class = [&]() {
         if (nc < 0) return;
         const int l2 = m.log2n[nc];
-        const int P = kMixNT * 2 * (l2 <= 10 ? m.bsmall : 4) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
+        const int P = kMixNT * 2 * mix_bins(l2, m.bsmall) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
         m.nseg[nc] = (int)segs;
         m.task0[nc] = (int)tasks;
         tasks += (segs + P - 1) / P;
@@ -1224,8 +1223,8 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     }
     m.n_tasks = (int)tasks;
     const int slot = (int)(g.exec_no++ % kMixSlots);
-    m.counter = g.ctr + 4 * slot;  // 16-B slots: the 64-bit counter of the two-ended order is 8-B aligned
-    m.done = g.ctr + 4 * slot + 2;
+    m.counter = g.ctr + 2 * slot;
+    m.done = g.ctr + 2 * slot + 1;
     const int grid = (int)std::min<int64_t>(res, tasks);
     HIP_OR(launch_slide_mix(m, nf, det, c0.f32, grid, s), MTB_INTERNAL_ERROR);
     return MTB_OK;
@@ -1841,9 +1840,9 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 9;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 7;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..9", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..7", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);
@@ -1962,8 +1961,8 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
     for (const Config &c : g->cfg)
         g->mix_ok = g->mix_ok && c.log2n >= 9 && c.log2n <= 12 && window_coef(c.window).nf <= 3;
     if (g->mix_ok) {
-        if (hipSetDevice(device) != hipSuccess || hipMalloc(&g->ctr, 4 * kMixSlots * sizeof(int)) != hipSuccess ||
-            hipMemset(g->ctr, 0, 4 * kMixSlots * sizeof(int)) != hipSuccess) {
+        if (hipSetDevice(device) != hipSuccess || hipMalloc(&g->ctr, 2 * kMixSlots * sizeof(int)) != hipSuccess ||
+            hipMemset(g->ctr, 0, 2 * kMixSlots * sizeof(int)) != hipSuccess) {
             set_error("wsp_group_create: task counters could not be allocated");
             return 0;
         }

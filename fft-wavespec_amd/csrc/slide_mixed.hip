@@ -5,9 +5,9 @@
 // Why one launch: as one launch per window length, every launch starts with all of its workgroups seeding at
 // once (in-LDS FFTs, no writes in flight) and ends with a drain, and small batches (a strong-scaled shard of
 // C5) pay both per length.  Here 512-thread workgroups, resident two per CU, pull tasks from a device counter:
-// task = one segment of a 4096-pt member, or two 2048 / two 1024 / four 512 segments side by side (sub-
+// task = one segment of a 4096-pt member, or two 2048 / two 1024 / eight 512 segments side by side (sub-
 // workgroups of N/(2B) threads, wave-aligned, so the workgroup barriers of the seed FFTs line up: every
-// sub-workgroup of a task has the same N).  Tasks are ordered longest windows first and each costs about the
+// sub-workgroup of a task has the same N; a 512-pt sub-workgroup is one wave and synchronises by wave fences).  Tasks are ordered longest windows first and each costs about the
 // same (S windows x 2048 bins, half that for N <= 1024), so after the first task the workgroups' seed phases
 // fall at different times and overlap the others' write streams, and the last tasks are the short ones.
 //
@@ -20,10 +20,22 @@
 namespace wsp {
 namespace {
 
+// Barrier of a sub-workgroup: the workgroup's (every sub-workgroup of a task runs the same N, so they line up), or,
+// when a sub-workgroup is one wave (WV), a wave fence -- LDS operations of one wave complete in order -- so the
+// task's waves run their segments independently instead of in lockstep.
+template <bool WV> __device__ __forceinline__ void sub_sync() {
+    if constexpr (WV) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 // In-place natural-order complex FFT of N points in LDS by the NT threads of a sub-workgroup (thread t): fft_lds
-// with the twiddles read from the W_4096 quarter table at stride 4096 / N.  Barriers are workgroup-wide: every
-// sub-workgroup of the workgroup runs the same N.
-template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf, const d2 *twq, int t) {
+// with the twiddles read from the W_4096 quarter table at stride 4096 / N.
+template <int LOG2N, int NT, bool WV = false> __device__ __forceinline__ void fft_lds_sub(d2 *buf, const d2 *twq, int t) {
     constexpr int N = 1 << LOG2N, H = N / 2, N4 = N / 4, TS = 4096 / N;
     int ns = 1;
     if constexpr (LOG2N & 1) {
@@ -34,14 +46,14 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
             a[q] = buf[t + NT * q];
             b[q] = buf[t + NT * q + H];
         }
-        __syncthreads();
+        sub_sync<WV>();
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int j = t + NT * q;
             buf[2 * j] = a[q] + b[q];
             buf[2 * j + 1] = a[q] - b[q];
         }
-        __syncthreads();
+        sub_sync<WV>();
         ns = 2;
     }
     constexpr int Q = N4 / NT;
@@ -56,7 +68,7 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * N4];
         }
-        __syncthreads();
+        sub_sync<WV>();
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int j = t + NT * q, k = j & (ns - 1);
@@ -70,7 +82,7 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
             buf[o + 2 * ns] = t0 - t2;
             buf[o + 3 * ns] = t1 - t3;
         }
-        __syncthreads();
+        sub_sync<WV>();
     }
 }
 
@@ -101,10 +113,12 @@ __device__ __forceinline__ bool mix_seg(MixP m, int c, int64_t s, const void *&s
 
 template <typename T, int LOG2N, int NF, int DETREND, int BS>
 __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq) {
-    // BS: bins per thread for N <= 1024 (4 by default: the short windows' tasks then hold 4 / 8 segments side by
-    // side, as many bins per thread-step as the long ones; 2 = the per-length launches' geometry, ablation)
-    constexpr int N = 1 << LOG2N, M = N / 2, B = LOG2N <= 10 ? BS : 4, NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
+    // bins per thread (mix_bins): 4 at N >= 2048; at N = 512 four, so that a 512-point sub-workgroup is ONE wave
+    // (WV): its seeds, uniforms and slide synchronise by wave fences and its trip count is its own segment's, where
+    // sub-workgroups of several waves keep workgroup barriers and run in lockstep; at N = 1024 two (BS = 4: four)
+    constexpr int N = 1 << LOG2N, M = N / 2, B = mix_bins(LOG2N, BS), NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
                   NM = (NF - 1) / 2;
+    constexpr bool WV = NT == 64;
     constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
     static_assert(P * N <= 4096 && CH * REC / 2 <= N && P * NT == kMixNT, "sub-workgroup geometry");
     // sub-workgroups are whole waves: the index (and the segment lookups below) are wave-uniform
@@ -119,7 +133,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     void *outp = m->out[0];
     const bool on = mix_seg(m, c, task * P + sub, ser, outp, w0, len);
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
+    for (int p = 0; p < (WV ? 0 : P); ++p) {
         const void *ps;
         void *po;
         int pl = 0;
@@ -148,8 +162,8 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
             const double xi = on ? (double)x[i] - lvl : 0.0;
             buf[i] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
         }
-        __syncthreads();
-        fft_lds_sub<LOG2N, NT>(buf, twq, t);
+        sub_sync<WV>();
+        fft_lds_sub<LOG2N, NT, WV>(buf, twq, t);
         const double s = mm == 0 ? m->s0 : (mm == 1 ? m->s1 : m->s2);
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -163,7 +177,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
             }
         }
         if (DETREND == kDetrendMean && mm == 0) sum = buf[0].x;  // sum of x - L
-        __syncthreads();
+        sub_sync<WV>();
     }
 #pragma unroll
     for (int b = 0; b < B; ++b)
@@ -180,11 +194,12 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     ua.s0 = m->s0, ua.s1 = m->s1, ua.s2 = m->s2, ua.c1 = c1, ua.sn1 = sn1, ua.c2 = c2, ua.sn2 = sn2;
     T *__restrict__ out = static_cast<T *>(outp) + w0 * M + 2 * t;
     double *u = reinterpret_cast<double *>(buf);
-    for (int c0 = 0; c0 < maxlen; c0 += CH) {
-        const int clen = maxlen - c0 < CH ? maxlen - c0 : CH;
-        if (c0) __syncthreads();
+    const int trip = WV ? len : maxlen;  // WV: this wave's own segment
+    for (int c0 = 0; c0 < trip; c0 += CH) {
+        const int clen = trip - c0 < CH ? trip - c0 : CH;
+        if (c0) sub_sync<WV>();
         stage_uniforms<T, NF, N>(ua, x, lvl, c0, clen < len - c0 ? clen : len - c0, len, u, t, NT);
-        __syncthreads();
+        sub_sync<WV>();
         const int act = len - c0 < clen ? (len - c0 > 0 ? len - c0 : 0) : clen;  // this sub-workgroup's windows
 #pragma unroll 1
         for (int st = 0; st < act; ++st) {
@@ -221,20 +236,7 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     for (int i = tid; i < 1024; i += kMixNT) twq[i] = tw[i];
     int *ldsi = reinterpret_cast<int *>(lds);
     for (;;) {
-        if (tid == 0) {
-            if (m->two_ended) {
-                // ablation (wsp_group_set_mode 3): every other group of 8 workgroups takes tasks from the end
-                // (shortest windows first), so concurrently running workgroups are at different phases (seed or
-                // slide) instead of all seeding at once; front + back < n_tasks decides on one 64-bit counter
-                const bool back = (blockIdx.x >> 3) & 1;
-                const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long *>(m->counter), back ? (1ull << 32) : 1ull);
-                const int f = (int)(old & 0xffffffffull), bk = (int)(old >> 32);
-                ldsi[0] = f + bk >= m->n_tasks ? m->n_tasks : (back ? m->n_tasks - 1 - bk : f);
-            } else {
-                ldsi[0] = atomicAdd(m->counter, 1);
-            }
-        }
+        if (tid == 0) ldsi[0] = atomicAdd(m->counter, 1);
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(ldsi[0]);  // uniform: the task's scalars stay in SGPRs
         __syncthreads();
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     if (tid == 0) {  // the last workgroup out resets this execute's counter slot
         __threadfence();
         if (atomicAdd(m->done, 1) == (int)gridDim.x - 1) {
-            atomicExch(reinterpret_cast<unsigned long long *>(m->counter), 0ull);  // both words of either order
+            atomicExch(m->counter, 0);
             atomicExch(m->done, 0);
         }
     }
@@ -302,16 +304,18 @@ template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, in
 }  // namespace
 
 int slide_mix_resident(int nf, int detrend, bool f32, int bsmall, int dev) {
+    if (bsmall == 1) return f32 ? resident_nf<float, 1>(nf, detrend, dev) : resident_nf<double, 1>(nf, detrend, dev);
     if (bsmall == 2) return f32 ? resident_nf<float, 2>(nf, detrend, dev) : resident_nf<double, 2>(nf, detrend, dev);
     return f32 ? resident_nf<float, 4>(nf, detrend, dev) : resident_nf<double, 4>(nf, detrend, dev);
 }
 
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t s) {
     if ((nf != 1 && nf != 3) || grid < 1 || m.nclass < 1 || m.nclass > kMixClass || m.n_tasks < 1 || !m.counter ||
-        !m.done || !m.tw4096 || (m.bsmall != 2 && m.bsmall != 4))
+        !m.done || !m.tw4096 || (m.bsmall != 1 && m.bsmall != 2 && m.bsmall != 4))
         return hipErrorInvalidValue;
     for (int c = 0; c < m.nclass; ++c)
         if (m.log2n[c] < 9 || m.log2n[c] > 12 || m.seg[c] < 1 || !m.omega[c]) return hipErrorInvalidValue;
+    if (m.bsmall == 1) return f32 ? launch_nf<float, 1>(m, nf, detrend, grid, s) : launch_nf<double, 1>(m, nf, detrend, grid, s);
     if (m.bsmall == 2) return f32 ? launch_nf<float, 2>(m, nf, detrend, grid, s) : launch_nf<double, 2>(m, nf, detrend, grid, s);
     return f32 ? launch_nf<float, 4>(m, nf, detrend, grid, s) : launch_nf<double, 4>(m, nf, detrend, grid, s);
 }

@@ -29,24 +29,11 @@ template <int LOG2L> struct LGeo {
     static_assert(LOG2L >= 6 && LOG2L <= 13, "transform length 64 .. 8192");
 };
 
-// Exchange barrier of wg_fft: the workgroup's, or (WAVE: every transform's TP threads lie in one wave, each
-// wave with LDS slots of its own) the wave's -- LDS operations of one wave complete in order, so a fence that
-// keeps the compiler from moving LDS accesses across it is all the wave needs, and the other waves run on
-template <bool WAVE> __device__ __forceinline__ void fft_sync() {
-    if constexpr (WAVE) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-        __syncthreads();
-    }
-}
-
 // L-point forward FFT of one transform held by TP threads (16 points each:
 // v[r] = x[t + TP r] on entry).  On exit v[q R + r] = X[b + (L/R) r] with
 // b = t + TP q and R the last pass's radix.  `slot` is this transform's LDS
 // region (SLOT elements); tw = W_N^j, j < N, of a table of period N (twN).
-template <typename T, int LOG2L, int PASS = 1, bool WAVE = false>
+template <typename T, int LOG2L, int PASS = 1>
 __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, const cpx<T> *__restrict__ tw, int log2tw) {
     using G = LGeo<LOG2L>;
     constexpr int L = G::L, TP = G::TP;
@@ -60,7 +47,7 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
 #pragma unroll
             for (int r = 0; r < Rp; ++r) slot[pad16(base + Nsp * r)] = v[q * Rp + r];
         }
-        fft_sync<WAVE>();
+        __syncthreads();
         constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
 #pragma unroll
         for (int q = 0; q < 16 / R; ++q) {
@@ -78,8 +65,8 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
             }
             dft<T, R>(v + q * R);
         }
-        fft_sync<WAVE>();  // slot reuse by the caller / next pass
-        wg_fft<T, LOG2L, PASS + 1, WAVE>(v, slot, t, tw, log2tw);
+        __syncthreads();  // slot reuse by the caller / next pass
+        wg_fft<T, LOG2L, PASS + 1>(v, slot, t, tw, log2tw);
     }
 }
 

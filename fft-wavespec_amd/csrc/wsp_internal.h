@@ -87,8 +87,7 @@ struct LargeLaunch {
                           // fp64 N = 65536, two passes otherwise), 1 two passes, 2 two passes pipelined over two streams,
                           // 3 fused (512 threads), 4 fused (256 threads, register prefetch), 5 fused with plain stores,
                           // 6 fp64 N = 262144 column pass at 16 columns per workgroup (default 8), 7 row pass in plain
-                          // block order (default XCD-aware), 8 fused with wave-local column FFTs, 9 with wave-local
-                          // rows as well
+                          // block order (default XCD-aware)
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,
@@ -164,21 +163,22 @@ constexpr int kMixClass = 4;   // window lengths 4096, 2048, 1024, 512
 constexpr int kMixNT = 512;    // threads per workgroup
 struct SlideMix {
     int nclass, n_tasks;
-    int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
-    int two_ended;                      // half the workgroups take tasks from the end (wsp_group_set_mode 3)
+    int bsmall;                         // geometry code of mix_bins: 2 (default), 4, 1 (wsp_group_set_mode 0 / 2 / 3)
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];
     double s0, s1, s2;                  // a0, a1/2, a2/2 of the (common) window
     const void *omega[kMixClass];       // slide table of class c (SlideArgs::omega)
     const void *tw4096;                 // W_4096^k, double complex: the quarter table of every length
-    int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup;
-                                        // counter 8-B aligned: 64-bit [front | back << 32] in the two-ended order)
+    int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup)
     int64_t sg0[kMixMax];               // member i: its first segment within its class
     int64_t n_windows[kMixMax];
     const void *series[kMixMax];
     void *out[kMixMax];
 };
+// Bins per thread of the mixed launch's class log2 N under geometry code bs: 4 at N >= 2048; N = 512: 4 (one-wave
+// sub-workgroups) unless bs == 1 (2: the round-3 per-length geometry, ablation); N = 1024: 4 if bs == 4, else 2.
+constexpr int mix_bins(int log2n, int bs) { return log2n >= 11 ? 4 : log2n == 9 ? (bs == 1 ? 2 : 4) : (bs == 4 ? 4 : 2); }
 // One launch of `grid` persistent workgroups (grid <= the resident count, slide_mix_resident).
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t stream);
 // Resident 512-thread workgroups of the mixed kernel on device `dev` (occupancy x CUs).

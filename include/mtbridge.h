@@ -298,7 +298,7 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
-/* Tuning / ablation: the kernel form, 0..9 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..7 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -312,8 +312,6 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    kernel with plain (not non-temporal) output stores; 6 = fp64 N = 262144
  *    with 16-column column-pass workgroups (the default takes 8); 7 = the
  *    two-pass row kernel in plain block order (the default is XCD-aware);
- *    8 = the fused kernel with wave-local column FFTs (N = 65536 / 131072);
- *    9 = the same with wave-local row FFTs and R2C pairs as well;
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
@@ -387,10 +385,10 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * most 32 members (workgroups pull segments of all lengths from a device
  * counter, longest windows first); otherwise one launch per window length.
  * 1 = one launch per window length (lanes: wsp_group_set_streams); 2 = the
- * mixed launch with four bins per thread at every length (ablation; the
- * default takes two for N <= 1024); 3 = the mixed launch with every other
- * group of 8 workgroups taking tasks from the end of the list (ablation).
- * MTB_BAD_ARGS outside 0..3. */
+ * mixed launch with four bins per thread at N = 1024 too (ablation; the
+ * default takes two there); 3 = the mixed launch with two bins per thread
+ * at N = 512 as well (two-wave sub-workgroups in lockstep; ablation; the
+ * default runs one-wave 512-point sub-workgroups).  MTB_BAD_ARGS outside 0..3. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
