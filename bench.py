@@ -71,10 +71,12 @@ def parse(argv=None):
     ap.add_argument("--c5-streams", type=int, default=0,
                     help="C5: lanes the grouped plan runs its launches on (wsp_group_set_streams; 0 = the library's "
                          "default, one per window length up to 4) / streams the symbol plans use (0 = 3)")
-    ap.add_argument("--c5-mode", default="group", choices=["group", "group-per-length", "group-mixed-b4", "group-mixed-lockstep", "plans"],
+    ap.add_argument("--c5-mode", default="group",
+                    choices=["group", "group-per-length", "group-mixed-b4", "group-mixed-lockstep", "plans"],
                     help="C5: one grouped device plan (wsp_group_*: one mixed-length persistent launch), the grouped "
-                         "plan's per-length launches on lanes (round-3 form), or one plan per symbol spread over "
-                         "--c5-streams streams (round-2 form)")
+                         "plan's per-length launches on lanes (round-3 form), the mixed launch's ablations (four bins "
+                         "per thread at N = 1024 / lockstep two-wave 512-point sub-workgroups: wsp_group_set_mode 2 / "
+                         "3), or one plan per symbol spread over --c5-streams streams (round-2 form)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-settle", action="store_true", help="skip the clock-settle phase (diagnostics)")
     ap.add_argument("--c5-shard", default="split", choices=["split", "split-time", "symbols"],
