@@ -1166,7 +1166,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     for (int i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
-    m.bsmall = g.mode == 2 ? 4 : g.mode == 3 ? 1 : 2;  // mix_bins; N = 1024 at 2: 0.737 ms against 0.777 (4), r04d
+    m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1187,7 +1187,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     auto close_class = [&]() {
         if (nc < 0) return;
         const int l2 = m.log2n[nc];
-        const int P = kMixNT * 2 * mix_bins(l2, m.bsmall) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
+        const int P = kMixNT * 2 * (l2 <= 10 ? m.bsmall : 4) / (1 << l2);  // sub-workgroups: 512 / (N / 2B)
         m.nseg[nc] = (int)segs;
         m.task0[nc] = (int)tasks;
         tasks += (segs + P - 1) / P;
@@ -2084,8 +2084,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 3) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..3", (long long)group, mode);
+    if (!g || mode < 0 || mode > 2) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..2", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

@@ -5,9 +5,9 @@
 // Why one launch: as one launch per window length, every launch starts with all of its workgroups seeding at
 // once (in-LDS FFTs, no writes in flight) and ends with a drain, and small batches (a strong-scaled shard of
 // C5) pay both per length.  Here 512-thread workgroups, resident two per CU, pull tasks from a device counter:
-// task = one segment of a 4096-pt member, or two 2048 / two 1024 / eight 512 segments side by side (sub-
+// task = one segment of a 4096-pt member, or two 2048 / two 1024 / four 512 segments side by side (sub-
 // workgroups of N/(2B) threads, wave-aligned, so the workgroup barriers of the seed FFTs line up: every
-// sub-workgroup of a task has the same N; a 512-pt sub-workgroup is one wave and synchronises by wave fences).  Tasks are ordered longest windows first and each costs about the
+// sub-workgroup of a task has the same N).  Tasks are ordered longest windows first and each costs about the
 // same (S windows x 2048 bins, half that for N <= 1024), so after the first task the workgroups' seed phases
 // fall at different times and overlap the others' write streams, and the last tasks are the short ones.
 //
@@ -20,22 +20,10 @@
 namespace wsp {
 namespace {
 
-// Barrier of a sub-workgroup: the workgroup's (every sub-workgroup of a task runs the same N, so they line up), or,
-// when a sub-workgroup is one wave (WV), a wave fence -- LDS operations of one wave complete in order -- so the
-// task's waves run their segments independently instead of in lockstep.
-template <bool WV> __device__ __forceinline__ void sub_sync() {
-    if constexpr (WV) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-        __syncthreads();
-    }
-}
-
 // In-place natural-order complex FFT of N points in LDS by the NT threads of a sub-workgroup (thread t): fft_lds
-// with the twiddles read from the W_4096 quarter table at stride 4096 / N.
-template <int LOG2N, int NT, bool WV = false> __device__ __forceinline__ void fft_lds_sub(d2 *buf, const d2 *twq, int t) {
+// with the twiddles read from the W_4096 quarter table at stride 4096 / N.  Barriers are workgroup-wide: every
+// sub-workgroup of the workgroup runs the same N.
+template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf, const d2 *twq, int t) {
     constexpr int N = 1 << LOG2N, H = N / 2, N4 = N / 4, TS = 4096 / N;
     int ns = 1;
     if constexpr (LOG2N & 1) {
@@ -46,14 +34,14 @@ template <int LOG2N, int NT, bool WV = false> __device__ __forceinline__ void ff
             a[q] = buf[t + NT * q];
             b[q] = buf[t + NT * q + H];
         }
-        sub_sync<WV>();
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int j = t + NT * q;
             buf[2 * j] = a[q] + b[q];
             buf[2 * j + 1] = a[q] - b[q];
         }
-        sub_sync<WV>();
+        __syncthreads();
         ns = 2;
     }
     constexpr int Q = N4 / NT;
@@ -68,7 +56,7 @@ template <int LOG2N, int NT, bool WV = false> __device__ __forceinline__ void ff
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * N4];
         }
-        sub_sync<WV>();
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int j = t + NT * q, k = j & (ns - 1);
@@ -82,7 +70,7 @@ template <int LOG2N, int NT, bool WV = false> __device__ __forceinline__ void ff
             buf[o + 2 * ns] = t0 - t2;
             buf[o + 3 * ns] = t1 - t3;
         }
-        sub_sync<WV>();
+        __syncthreads();
     }
 }
 
@@ -113,12 +101,12 @@ __device__ __forceinline__ bool mix_seg(MixP m, int c, int64_t s, const void *&s
 
 template <typename T, int LOG2N, int NF, int DETREND, int BS>
 __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq) {
-    // bins per thread (mix_bins): 4 at N >= 2048; at N = 512 four, so that a 512-point sub-workgroup is ONE wave
-    // (WV): its seeds, uniforms and slide synchronise by wave fences and its trip count is its own segment's, where
-    // sub-workgroups of several waves keep workgroup barriers and run in lockstep; at N = 1024 two (BS = 4: four)
-    constexpr int N = 1 << LOG2N, M = N / 2, B = mix_bins(LOG2N, BS), NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
+    // BS: bins per thread for N <= 1024 (2 by default, the per-length launches' geometry: 0.737 against 0.777 ms
+    // for C5 at 4, which holds 4 / 8 segments side by side; profiles/r04/ab).  One-wave 512-point sub-workgroups
+    // with wave fences instead of lockstep barriers lost too (0.812 against 0.735 ms: the N = 512 tail then has
+    // half the tasks, tools/ablations/c5_mixed_one_wave_512.patch)
+    constexpr int N = 1 << LOG2N, M = N / 2, B = LOG2N <= 10 ? BS : 4, NT = M / B, P = kMixNT / NT, REC = Rec<NF>::n,
                   NM = (NF - 1) / 2;
-    constexpr bool WV = NT == 64;
     constexpr int CH = N / 4 < 128 ? 128 : (N / 4 > kSlideRMax ? kSlideRMax : N / 4);
     static_assert(P * N <= 4096 && CH * REC / 2 <= N && P * NT == kMixNT, "sub-workgroup geometry");
     // sub-workgroups are whole waves: the index (and the segment lookups below) are wave-uniform
@@ -133,7 +121,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     void *outp = m->out[0];
     const bool on = mix_seg(m, c, task * P + sub, ser, outp, w0, len);
 #pragma unroll
-    for (int p = 0; p < (WV ? 0 : P); ++p) {
+    for (int p = 0; p < P; ++p) {
         const void *ps;
         void *po;
         int pl = 0;
@@ -162,8 +150,8 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
             const double xi = on ? (double)x[i] - lvl : 0.0;
             buf[i] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
         }
-        sub_sync<WV>();
-        fft_lds_sub<LOG2N, NT, WV>(buf, twq, t);
+        __syncthreads();
+        fft_lds_sub<LOG2N, NT>(buf, twq, t);
         const double s = mm == 0 ? m->s0 : (mm == 1 ? m->s1 : m->s2);
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -177,7 +165,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
             }
         }
         if (DETREND == kDetrendMean && mm == 0) sum = buf[0].x;  // sum of x - L
-        sub_sync<WV>();
+        __syncthreads();
     }
 #pragma unroll
     for (int b = 0; b < B; ++b)
@@ -194,12 +182,11 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     ua.s0 = m->s0, ua.s1 = m->s1, ua.s2 = m->s2, ua.c1 = c1, ua.sn1 = sn1, ua.c2 = c2, ua.sn2 = sn2;
     T *__restrict__ out = static_cast<T *>(outp) + w0 * M + 2 * t;
     double *u = reinterpret_cast<double *>(buf);
-    const int trip = WV ? len : maxlen;  // WV: this wave's own segment
-    for (int c0 = 0; c0 < trip; c0 += CH) {
-        const int clen = trip - c0 < CH ? trip - c0 : CH;
-        if (c0) sub_sync<WV>();
+    for (int c0 = 0; c0 < maxlen; c0 += CH) {
+        const int clen = maxlen - c0 < CH ? maxlen - c0 : CH;
+        if (c0) __syncthreads();
         stage_uniforms<T, NF, N>(ua, x, lvl, c0, clen < len - c0 ? clen : len - c0, len, u, t, NT);
-        sub_sync<WV>();
+        __syncthreads();
         const int act = len - c0 < clen ? (len - c0 > 0 ? len - c0 : 0) : clen;  // this sub-workgroup's windows
 #pragma unroll 1
         for (int st = 0; st < act; ++st) {
@@ -304,18 +291,16 @@ template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, in
 }  // namespace
 
 int slide_mix_resident(int nf, int detrend, bool f32, int bsmall, int dev) {
-    if (bsmall == 1) return f32 ? resident_nf<float, 1>(nf, detrend, dev) : resident_nf<double, 1>(nf, detrend, dev);
     if (bsmall == 2) return f32 ? resident_nf<float, 2>(nf, detrend, dev) : resident_nf<double, 2>(nf, detrend, dev);
     return f32 ? resident_nf<float, 4>(nf, detrend, dev) : resident_nf<double, 4>(nf, detrend, dev);
 }
 
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t s) {
     if ((nf != 1 && nf != 3) || grid < 1 || m.nclass < 1 || m.nclass > kMixClass || m.n_tasks < 1 || !m.counter ||
-        !m.done || !m.tw4096 || (m.bsmall != 1 && m.bsmall != 2 && m.bsmall != 4))
+        !m.done || !m.tw4096 || (m.bsmall != 2 && m.bsmall != 4))
         return hipErrorInvalidValue;
     for (int c = 0; c < m.nclass; ++c)
         if (m.log2n[c] < 9 || m.log2n[c] > 12 || m.seg[c] < 1 || !m.omega[c]) return hipErrorInvalidValue;
-    if (m.bsmall == 1) return f32 ? launch_nf<float, 1>(m, nf, detrend, grid, s) : launch_nf<double, 1>(m, nf, detrend, grid, s);
     if (m.bsmall == 2) return f32 ? launch_nf<float, 2>(m, nf, detrend, grid, s) : launch_nf<double, 2>(m, nf, detrend, grid, s);
     return f32 ? launch_nf<float, 4>(m, nf, detrend, grid, s) : launch_nf<double, 4>(m, nf, detrend, grid, s);
 }

@@ -163,7 +163,7 @@ constexpr int kMixClass = 4;   // window lengths 4096, 2048, 1024, 512
 constexpr int kMixNT = 512;    // threads per workgroup
 struct SlideMix {
     int nclass, n_tasks;
-    int bsmall;                         // geometry code of mix_bins: 2 (default), 4, 1 (wsp_group_set_mode 0 / 2 / 3)
+    int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];
@@ -176,9 +176,6 @@ struct SlideMix {
     const void *series[kMixMax];
     void *out[kMixMax];
 };
-// Bins per thread of the mixed launch's class log2 N under geometry code bs: 4 at N >= 2048; N = 512: 4 (one-wave
-// sub-workgroups) unless bs == 1 (2: the round-3 per-length geometry, ablation); N = 1024: 4 if bs == 4, else 2.
-constexpr int mix_bins(int log2n, int bs) { return log2n >= 11 ? 4 : log2n == 9 ? (bs == 1 ? 2 : 4) : (bs == 4 ? 4 : 2); }
 // One launch of `grid` persistent workgroups (grid <= the resident count, slide_mix_resident).
 hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, int grid, hipStream_t stream);
 // Resident 512-thread workgroups of the mixed kernel on device `dev` (occupancy x CUs).

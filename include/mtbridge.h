@@ -385,10 +385,8 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * most 32 members (workgroups pull segments of all lengths from a device
  * counter, longest windows first); otherwise one launch per window length.
  * 1 = one launch per window length (lanes: wsp_group_set_streams); 2 = the
- * mixed launch with four bins per thread at N = 1024 too (ablation; the
- * default takes two there); 3 = the mixed launch with two bins per thread
- * at N = 512 as well (two-wave sub-workgroups in lockstep; ablation; the
- * default runs one-wave 512-point sub-workgroups).  MTB_BAD_ARGS outside 0..3. */
+ * mixed launch with four bins per thread for N <= 1024 (ablation; the
+ * default takes two there).  MTB_BAD_ARGS outside 0..2. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
