@@ -53,6 +53,19 @@ template <typename T> __device__ __forceinline__ cpx<T> cmul(cpx<T> a, cpx<T> b)
 }
 template <typename T> __device__ __forceinline__ cpx<T> cconj(cpx<T> a) { return {a.re, -a.im}; }
 
+// fp32: complex arithmetic on (re, im) register pairs as packed fp32 (v_pk_add / v_pk_mul / v_pk_fma_f32, the
+// swaps and negations folded into op_sel / neg modifiers): one instruction per complex add and two per multiply
+// instead of 2 and 4, and no v_mov to assemble the pairs the vectoriser otherwise forms ad hoc (the fp32 spectrum
+// kernel is VALU-issue-bound: 0.97 of the issue slots, profiles/r04/sq/c3_sq_counters.csv)
+__device__ __forceinline__ f2v pk(cpx<float> a) { return __builtin_bit_cast(f2v, a); }
+__device__ __forceinline__ cpx<float> unpk(f2v a) { return __builtin_bit_cast(cpx<float>, a); }
+template <> __device__ __forceinline__ cpx<float> cadd(cpx<float> a, cpx<float> b) { return unpk(pk(a) + pk(b)); }
+template <> __device__ __forceinline__ cpx<float> csub(cpx<float> a, cpx<float> b) { return unpk(pk(a) - pk(b)); }
+template <> __device__ __forceinline__ cpx<float> cmul(cpx<float> a, cpx<float> b) {
+    const f2v A = pk(a), Bv = pk(b);
+    return unpk(__builtin_elementwise_fma(A.yy, f2v{-Bv.y, Bv.x}, A.xx * Bv));
+}
+
 // cos(2 pi k/16); sin(2 pi k/16) = cos16(k - 4).
 __host__ __device__ constexpr double cos16(int k) {
     constexpr double C1 = 0.92387953251128675613, C2 = 0.70710678118654752440, C3 = 0.38268343236508977173;
@@ -68,6 +81,21 @@ __host__ __device__ constexpr double sin16(int k) { return cos16(k - 4); }
 // a * W16^k, W16 = e^{-2 pi i/16}; k is a compile-time constant after
 // unrolling, so the switch folds and trivial factors cost no multiply.
 template <typename T> __device__ __forceinline__ cpx<T> mulw16(cpx<T> a, int k) {
+    if constexpr (std::is_same_v<T, float>) {  // packed: a c + (a.im, -a.re) s
+        const f2v A = pk(a), J = f2v{A.y, -A.x};
+        const float h = 0.70710678118654752440f;
+        switch (k & 15) {
+        case 0: return a;
+        case 4: return unpk(J);
+        case 8: return unpk(-A);
+        case 12: return unpk(-J);
+        case 2: return unpk((A + J) * h);
+        case 6: return unpk((J - A) * h);
+        case 10: return unpk((-A - J) * h);
+        case 14: return unpk((A - J) * h);
+        default: return unpk(__builtin_elementwise_fma(A, f2v{float(cos16(k)), float(cos16(k))}, J * float(sin16(k))));
+        }
+    }
     const T h = T(0.70710678118654752440);
     switch (k & 15) {
     case 0: return a;
