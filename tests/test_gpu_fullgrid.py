@@ -397,3 +397,89 @@ def test_c5_grouped_plan(gpu_session):
         plan.close()
     _record("c5_group", symbols=28, rel_err=worst)
     g.close()
+
+
+def test_c2_full_size(gpu_session):
+    """C2 at its benchmarked size (4096 x 1024, hop = 1024, fp64 Hann: spectrum_kernel<double,10,...>, one
+    grid-stride iteration): every window against torch.fft with the reference's symmetric Hann, and sampled
+    windows against the oracle."""
+    torch = pytest.importorskip("torch")
+    n, w = 1024, 4096
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 17, dev)
+    d_o = torch.empty(w * n // 2, dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    X = d_s.view(w, n)
+    hann = 0.5 * (1 - torch.cos(2 * np.pi * torch.arange(n, device=dev, dtype=torch.float64) / (n - 1)))
+    F = torch.fft.rfft(X * hann, dim=1)[:, : n // 2]
+    Pt = F.real ** 2 + F.imag ** 2
+    err = ((P - Pt).abs().amax(dim=1) / Pt.abs().amax(dim=1)).max().item()
+    assert err < 1e-12, err
+    idx, _ = _sample(w, 2, seed=9)
+    host = X[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    got = P[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.stack([oracle.window_spectrum(x, "none", "hann") for x in host])
+    _check_power("c2", got, want, n, 1e-10)
+    plan.close()
+
+
+@pytest.mark.parametrize("n,w", [(65536, 4096), (262144, 1024)])
+def test_large_full_batches(gpu_session, n, w):
+    """The benchmarked large-N batches through the default forms (fused one-workgroup-per-window kernel at
+    N = 65536; two passes at N = 262144 with 8-column column workgroups and the XCD-aware row order): every
+    window against torch.fft with the symmetric Hann (max error relative to the window's largest bin), and the
+    first, last and two middle windows -- one of them in the last chunk -- against the oracle."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 23, dev)
+    d_o = torch.empty(w * (n // 2), dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = d_o.view(w, n // 2)
+    X = d_s.view(w, n)
+    hann = 0.5 * (1 - torch.cos(2 * np.pi * torch.arange(n, device=dev, dtype=torch.float64) / (n - 1)))
+    err = 0.0
+    for c0 in range(0, w, 64):
+        F = torch.fft.rfft(X[c0:c0 + 64] * hann, dim=1)[:, : n // 2]
+        Pt = F.real ** 2 + F.imag ** 2
+        err = max(err, ((P[c0:c0 + 64] - Pt).abs().amax(dim=1) / Pt.abs().amax(dim=1)).max().item())
+    assert err < 1e-11, err
+    idx = np.array([0, w // 3, w - 37, w - 1])
+    host = X[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    got = P[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.stack([oracle.window_spectrum(x, "none", "hann") for x in host])
+    _check_power(f"large_{n}", got, want, n, 1e-10)
+    _record(f"large_{n}_vs_torch", windows=w, max_rel_err=err)
+    plan.close()
+
+
+def test_ns_phase_full_grid(gpu_session):
+    """The benchmarked phase record (ns_phase: 65536 x 4096 fp64 Hann -> [P | unwrapped phase | group delay]):
+    sampled windows from both grid-stride iterations against the oracle with the parity suite's near-tie
+    conditioning of the unwrap decisions."""
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import _delay_match, _unwrap_match
+    n, w = 4096, 65536
+    dev = torch.device("cuda", 0)
+    d_s = synth.random_walk_torch(n * w, 29, dev)
+    d_o = torch.empty(w * 3 * (n // 2), dtype=torch.float64, device=dev)
+    plan = bridge.Plan(0, n, n, w, "none", "hann", output="phase")
+    plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    R = d_o.view(w, 3, n // 2)
+    idx, iters = _sample(w, 1, k=12, seed=31)
+    assert iters == 2
+    host = d_s.view(w, n)[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    got = R[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    want = np.concatenate([oracle.batch_phase(x, n, n, "none", "hann") for x in host])
+    assert oracle.rel_err(got[:, 0], want[:, 0]) <= 1e-10
+    for i in range(len(idx)):
+        mag = np.sqrt(want[i, 0])
+        m = _unwrap_match(got[i, 1], want[i, 1], mag)
+        _delay_match(got[i, 2], want[i, 2], mag, m)
+    _record("ns_phase", windows=len(idx))
+    plan.close()
