@@ -747,6 +747,7 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
             const double mwv = DETREND == kDetrendMean ? sum * a.inv_n : 0.0;
             d2 X[NB];
             int ph[NB];  // high words of the powers (non-negative doubles order as their bits); INT_MIN outside
+            int mh = 0x7fffffff;
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 d2 v = tr[b][0];
@@ -756,23 +757,9 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
                 X[b] = v;
                 const double p = v.x * v.x + v.y * v.y;
                 ph[b] = l + 64 * b < span ? (int)(__builtin_bit_cast(unsigned long long, p) >> 32) : INT_MIN;
+                if ((mask[b] >> slot) & 1u) mh = min(mh, ph[b]);
             }
-            // tau's high word: the min over this slot's probe lanes (<= k of them), read lane by lane into scalar
-            // registers (one v_readlane each, the min in SALU) instead of a 64-lane DPP / permlane reduction
-            int th = 0;
-            if (wi > 0 && probes) {
-                int m = 0x7fffffff;
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    unsigned long long pm = __ballot((mask[b] >> slot) & 1u);
-                    while (pm) {
-                        const int ln = __builtin_ctzll(pm);
-                        pm &= pm - 1;
-                        m = min(m, __builtin_amdgcn_readlane(ph[b], ln));
-                    }
-                }
-                th = m;
-            }
+            const int th = (wi > 0 && probes) ? core::wave_min64(mh) : 0;
             unsigned long long bal[NB];
             int total = 0;
 #pragma unroll
