@@ -4,5 +4,5 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-bash scripts/gpu_run.sh r04final tests smoke default bench=north_star bench=c2 bench=c3 bench=c4 bench=c4_topk bench=c5 \
+bash scripts/gpu_run.sh ${TAG:-r04final} tests smoke default bench=north_star bench=c2 bench=c3 bench=c4 bench=c4_topk bench=c5 \
     bench=ns_topk bench=ns_phase bench=ns_topk_phase bench=inverse bench=large bench=large_262144 prof=north_star
