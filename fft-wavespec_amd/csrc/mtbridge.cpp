@@ -1174,10 +1174,15 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     int64_t bins = 0;
     for (const Config &c : g.cfg) bins += c.n_windows * (int64_t)(c.n / 2);
     int64_t S = g.seg;
-    if (S <= 0) {
+    const bool policy = S <= 0;
+    if (policy) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
         S = std::min<int64_t>(256, std::max<int64_t>(128, S));
     }
+    // the last class (the shortest windows, picked up last) drains the launch: half-length segments there, so
+    // its tasks are finer and the workgroups finish closer together (mode 3: one length for every class, A/B)
+    const int last_l2 = g.cfg[order[n - 1]].log2n;
+    const bool tail_half = policy && g.mode != 3 && g.cfg[order[0]].log2n != last_l2;
     Tables t4096;
     int st = get_tables(g.dev, 12, false, &t4096);
     if (st != MTB_OK) return st;
@@ -1201,7 +1206,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
             SlideArgs A{};
             if ((st = slide_args(g.dev, c, &A)) != MTB_OK) return st;
             m.log2n[nc] = c.log2n;
-            m.seg[nc] = (int)S;
+            m.seg[nc] = (int)(tail_half && c.log2n == last_l2 ? std::max<int64_t>(64, S / 2) : S);
             m.mem0[nc] = i;
             m.c1[nc] = A.c1, m.sn1[nc] = A.sn1, m.c2[nc] = A.c2, m.sn2[nc] = A.sn2, m.inv_n[nc] = A.inv_n;
             m.omega[nc] = A.omega;
@@ -1212,7 +1217,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
         m.n_windows[i] = c.n_windows;
         m.series[i] = d_series[order[i]];
         m.out[i] = d_out[order[i]];
-        segs += (c.n_windows + S - 1) / S;
+        segs += (c.n_windows + m.seg[nc] - 1) / m.seg[nc];
     }
     close_class();
     m.nclass = nc + 1;
@@ -2084,8 +2089,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 2) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..2", (long long)group, mode);
+    if (!g || mode < 0 || mode > 3) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..3", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

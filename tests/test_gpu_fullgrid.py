@@ -387,7 +387,7 @@ def test_c5_grouped_plan(gpu_session):
         assert torch.isfinite(P).all().item()
         # seams of the per-length policy's lengths, and of the mixed launch's (~two tasks per resident workgroup:
         # 459.6M bins / (2 x 512 x 2048) = 220 windows at 512 resident workgroups)
-        seams = np.concatenate([[k * sg - 1, k * sg] for sg in (32, 64, 128, 256, *range(200, 241)) for k in (1, nw // sg)])
+        seams = np.concatenate([[k * sg - 1, k * sg] for sg in (32, 64, 128, 256, *range(100, 121), *range(200, 241)) for k in (1, nw // sg)])
         idx = np.unique(np.clip(np.r_[0, 1, nw - 2, nw - 1, rng.integers(0, nw, 6), seams], 0, nw - 1))
         x = series[s].cpu().numpy()
         want = np.stack([oracle.window_spectrum(x[i:i + n], "none", "hann") for i in idx])
