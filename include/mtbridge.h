@@ -386,9 +386,10 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * counter, longest windows first); otherwise one launch per window length.
  * 1 = one launch per window length (lanes: wsp_group_set_streams); 2 = the
  * mixed launch with four bins per thread for N <= 1024 (ablation; the
- * default takes two there); 3 = the mixed launch with one segment length
- * for every window length (ablation; the default halves the segments of
- * the shortest length, which drains the launch).  MTB_BAD_ARGS outside 0..3. */
+ * default takes two there); 3 = the mixed launch with half-length segments
+ * for the shortest window length, which drains the launch (ablation; the
+ * default uses one segment length for every window length).  MTB_BAD_ARGS
+ * outside 0..3. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
