@@ -583,6 +583,8 @@ template <typename T, int LM1, int LM2, int WC, bool MEAN>
 hipError_t col_launch(const large::ColArgs &a, int variant, hipStream_t s) {
     if constexpr (LM2 == 9 && sizeof(T) == 8)
         if (variant != 6) return col_launch_cb<T, LM1, LM2, WC, MEAN, 8>(a, s);
+    if constexpr (LM2 == 8 && sizeof(T) == 8)  // variant 8: the same 8-column form at M2 = 256 (N = 65536, two passes)
+        if (variant == 8) return col_launch_cb<T, LM1, LM2, WC, MEAN, 8>(a, s);
     return col_launch_cb<T, LM1, LM2, WC, MEAN>(a, s);
 }
 

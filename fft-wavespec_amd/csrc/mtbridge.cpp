@@ -1845,7 +1845,7 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 7;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
         set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..7", (long long)plan, variant);
         return MTB_BAD_ARGS;

@@ -87,7 +87,7 @@ struct LargeLaunch {
                           // fp64 N = 65536, two passes otherwise), 1 two passes, 2 two passes pipelined over two streams,
                           // 3 fused (512 threads), 4 fused (256 threads, register prefetch), 5 fused with plain stores,
                           // 6 fp64 N = 262144 column pass at 16 columns per workgroup (default 8), 7 row pass in plain
-                          // block order (default XCD-aware)
+                          // block order (default XCD-aware), 8 two passes with 8-column column workgroups at M2 = 256
 };
 hipError_t launch_large(const LargeLaunch &L, hipStream_t stream);
 // windows per chunk: about 192 MiB of column results (measured best of 16..2048 MiB,

@@ -312,6 +312,8 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    kernel with plain (not non-temporal) output stores; 6 = fp64 N = 262144
  *    with 16-column column-pass workgroups (the default takes 8); 7 = the
  *    two-pass row kernel in plain block order (the default is XCD-aware);
+ *    8 = two passes with 8-column column-pass workgroups at M2 = 256 (fp64
+ *    N = 65536 / 131072);
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the

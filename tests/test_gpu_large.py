@@ -158,14 +158,16 @@ def test_large_device_plan(gpu_session):
     (65536, 4, "none", "hann", "power"), (65536, 5, "mean", "hann", "power"), (131072, 3, "none", "bartlett", "power"),
     (131072, 2, "iir", "hann", "power"), (262144, 6, "none", "hann", "power"), (262144, 6, "mean", "blackman", "packed"),
     (262144, 7, "none", "hann", "power"), (32768, 7, "iir", "bartlett", "packed"),
-    (32768, 2, "mean", "hamming", "power")])
+    (32768, 2, "mean", "hamming", "power"), (65536, 8, "none", "hann", "power"), (65536, 8, "mean", "blackman", "packed"),
+    (131072, 8, "iir", "hamming", "power")])
 def test_large_variants_identical(gpu_session, n, variant, detrend, window, output):
     """The large-N kernel forms (wsp_plan_set_variant) against the two-pass form (variant 1): 0 = the library's
     choice (the fused kernel for fp64 N = 65536), 2 = two-pass over quarter chunks pipelined on two internal
     streams, 3 = the fused one-workgroup-per-window kernel at 512 threads, 4 = the same at 256 threads with
     register prefetch, 5 = the fused kernel with plain output stores, 6 = N = 262144's column pass at 16 columns
     per workgroup (the default takes 8), 7 = the two-pass row kernel in plain block order (the default maps blocks
-    XCD-aware).  They run the same arithmetic: identical records (variants 2, 6 and 7) or
+    XCD-aware), 8 = two passes with 8-column column workgroups at M2 = 256 (N = 65536 / 131072).  They run the
+    same arithmetic: identical records (variants 2, 6, 7 and 8) or
     within 1e-13 (the fused kernel: the same operations, contracted differently by the
     compiler; its window angles by rotation across column blocks), and the oracle's bar."""
     torch = pytest.importorskip("torch")
@@ -183,7 +185,7 @@ def test_large_variants_identical(gpu_session, n, variant, detrend, window, outp
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy().reshape(nwin, plan.record))
         plan.close()
-    if variant in (2, 6, 7):  # the same per-column arithmetic over other chunk boundaries / workgroup shapes: identical
+    if variant in (2, 6, 7, 8):  # the same per-column arithmetic over other chunk boundaries / workgroup shapes: identical
         assert np.array_equal(outs[0], outs[1])
     else:
         den = np.abs(outs[0]).max(axis=1, keepdims=True)
