@@ -1,5 +1,7 @@
 # round-4 session check l: half-length segments for the mixed C5 launch's last class (the shortest windows, which
 # drain the launch) against one segment length for every class (mode 3); group tests first.
+# (As run at commit 0a9c387, where tail-half was the default and mode 3 "mixed-uniform" the one-length ablation;
+# since b47fafe one length is the default and mode 3 is "mixed-tail-half", so this script no longer runs as is.)
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
