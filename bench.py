@@ -50,7 +50,7 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "FFT-windows/sec"
 CONFIGS = ["c2", "c3", "north_star", "c4", "c4_topk", "c5", "ns_topk", "ns_phase", "ns_topk_phase", "inverse", "large",
-           "large_262144"]
+           "large_131072", "large_262144"]
 
 
 def parse(argv=None):

@@ -57,6 +57,7 @@ CONFIGS = {
                     output="inverse"),
     # the legacy default InpFFTWindow = 65536 (four-step path), north-star bytes
     "large": dict(windows=4096, n=65536, hop=65536, precision="f64", detrend="none", window="hann", seed=11),
+    "large_131072": dict(windows=2048, n=131072, hop=131072, precision="f64", detrend="none", window="hann", seed=11),
     "large_262144": dict(windows=1024, n=262144, hop=262144, precision="f64", detrend="none", window="hann", seed=11),
 }
 

@@ -431,10 +431,11 @@ def test_c2_full_size(gpu_session):
     plan.close()
 
 
-@pytest.mark.parametrize("n,w", [(65536, 4096), (262144, 1024)])
+@pytest.mark.parametrize("n,w", [(65536, 4096), (131072, 2048), (262144, 1024)])
 def test_large_full_batches(gpu_session, n, w):
     """The benchmarked large-N batches through the default forms (fused one-workgroup-per-window kernel at
-    N = 65536; two passes at N = 262144 with 8-column column workgroups and the XCD-aware row order): every
+    N = 65536; two passes at N = 131072 and at N = 262144 with 8-column column workgroups and the XCD-aware row
+    order there): every
     window against numpy's FFT on the host with the symmetric Hann (max error relative to the window's largest
     bin), and the first, last and two middle windows -- one of them in the last chunk -- against the oracle."""
     torch = pytest.importorskip("torch")
