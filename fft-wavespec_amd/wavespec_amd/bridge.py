@@ -391,7 +391,9 @@ class Group:
     MODES = {"auto": 0, "per-length": 1, "mixed-b4": 2, "mixed-tail-half": 3}
 
     def set_mode(self, mode: str) -> None:
-        """"auto": one mixed-length persistent launch where eligible; "per-length": one launch per window length."""
+        """"auto": one mixed-length persistent launch where eligible; "per-length": one launch per window length;
+        "mixed-b4" / "mixed-tail-half": ablations of the mixed launch (four bins per thread for N <= 1024 /
+        half-length segments for the shortest window length) -- wsp_group_set_mode 0..3, include/mtbridge.h."""
         _check("wsp_group_set_mode", lib().wsp_group_set_mode(self.handle, self.MODES[mode]))
 
     def execute(self, d_series, d_out, stream: int = 0) -> None:
