@@ -1175,14 +1175,19 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     for (const Config &c : g.cfg) bins += c.n_windows * (int64_t)(c.n / 2);
     int64_t S = g.seg;
     const bool policy = S <= 0;
+    bool above_floor = false;
     if (policy) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
+        above_floor = S > 128;
         S = std::min<int64_t>(256, std::max<int64_t>(128, S));
     }
-    // mode 3 (ablation): half-length segments for the last class (the shortest windows, picked up last, drain
-    // the launch) -- r04l: 0.7 % faster on the full C5 batch, 5 % slower on a 1/8 shard, so one length is the default
+    // Half-length segments for the last class (the shortest windows, picked up last, drain the launch) when the
+    // batch is large enough that the policy's segments are above the floor: the full C5 batch 0.7322-0.7325 ms
+    // against 0.7373-0.7398 with one length on three boxes (r04l, r04m), while a one-eighth shard (segments at the
+    // floor, where halving only adds seeds) ran 5 % slower with them.  Mode 3: at every size; mode 4: never (A/B).
     const int last_l2 = g.cfg[order[n - 1]].log2n;
-    const bool tail_half = policy && g.mode == 3 && g.cfg[order[0]].log2n != last_l2;
+    const bool tail_half = policy && g.cfg[order[0]].log2n != last_l2 &&
+                           (g.mode == 3 || ((g.mode == 0 || g.mode == 2) && above_floor));
     Tables t4096;
     int st = get_tables(g.dev, 12, false, &t4096);
     if (st != MTB_OK) return st;
@@ -2089,8 +2094,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 3) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..3", (long long)group, mode);
+    if (!g || mode < 0 || mode > 4) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..4", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

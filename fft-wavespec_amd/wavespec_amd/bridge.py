@@ -388,12 +388,13 @@ class Group:
         """Tuning: windows per sliding-DFT workgroup (0 = the launcher's policy)."""
         _check("wsp_group_set_segment", lib().wsp_group_set_segment(self.handle, windows))
 
-    MODES = {"auto": 0, "per-length": 1, "mixed-b4": 2, "mixed-tail-half": 3}
+    MODES = {"auto": 0, "per-length": 1, "mixed-b4": 2, "mixed-tail-half": 3, "mixed-uniform": 4}
 
     def set_mode(self, mode: str) -> None:
         """"auto": one mixed-length persistent launch where eligible; "per-length": one launch per window length;
-        "mixed-b4" / "mixed-tail-half": ablations of the mixed launch (four bins per thread for N <= 1024 /
-        half-length segments for the shortest window length) -- wsp_group_set_mode 0..3, include/mtbridge.h."""
+        "mixed-b4" / "mixed-tail-half" / "mixed-uniform": ablations of the mixed launch (four bins per thread for
+        N <= 1024 / half-length segments for the shortest window length at every batch size / never) --
+        wsp_group_set_mode 0..4, include/mtbridge.h."""
         _check("wsp_group_set_mode", lib().wsp_group_set_mode(self.handle, self.MODES[mode]))
 
     def execute(self, d_series, d_out, stream: int = 0) -> None:

@@ -389,9 +389,11 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * 1 = one launch per window length (lanes: wsp_group_set_streams); 2 = the
  * mixed launch with four bins per thread for N <= 1024 (ablation; the
  * default takes two there); 3 = the mixed launch with half-length segments
- * for the shortest window length, which drains the launch (ablation; the
- * default uses one segment length for every window length).  MTB_BAD_ARGS
- * outside 0..3. */
+ * for the shortest window length, which drains the launch, at every batch
+ * size (the default does so only when the batch is large enough that the
+ * segment policy is above its floor of 128 windows); 4 = the mixed launch
+ * with one segment length for every window length (ablation).  MTB_BAD_ARGS
+ * outside 0..4. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
