@@ -771,7 +771,10 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     if (L.variant == 4 && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7, 256, true>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8, 256, true>(L, ca, ra, wclass, means != nullptr, s);
-    if (L.variant == 2) return pipelined_t<T>(L, ca, ra, wclass, means != nullptr, log2m, s);
+    // the pipelined form alternates two Y buffers of max(1, chunk / 4) windows: it needs the workspace to hold
+    // two of them, which a one-window chunk (wsp_plan_set_chunk(plan, 1)) does not -- that plan runs the
+    // plain chunk loop below instead of writing a second buffer past its workspace
+    if (L.variant == 2 && L.chunk >= 2) return pipelined_t<T>(L, ca, ra, wclass, means != nullptr, log2m, s);
     for (int64_t w0 = 0; w0 < L.n_windows; w0 += L.chunk) {
         ca.w0 = ra.w0 = w0;
         ca.nwin = ra.nwin = std::min<int64_t>(L.chunk, L.n_windows - w0);

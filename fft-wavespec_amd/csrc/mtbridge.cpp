@@ -681,26 +681,91 @@ struct LiveCtx {
 // price bars into pinned host buffers for hipMemcpyAsync").  A registered fp64 series is DMA'd to
 // the device from where it lies, and a registered output array receives the D2H copy directly:
 // no staging copy on either side of a synchronous batch.  Held by the session, released with it.
+//
+// Only WHOLE PAGES INSIDE the caller's buffer are page-locked (round 5): [a, a + bytes) registers
+// [round_up(a), round_down(a + bytes)), page-exact, and the < 1-page head and tail outside that span go
+// through a small pinned bounce buffer per batch.  A caller's heap array shares its first and last page
+// with other heap objects; page-locking those pages (which hipHostRegister does for any byte range, the
+// pinning granularity is the page) left the runtime holding host-pointer mappings over memory the
+// library does not own, and page-sharing registrations of neighbouring arrays overlapped in those pages
+// (the round-4 illegal-address faults).  With page-exact spans inside disjoint caller
+// buffers no page is ever locked that holds anything but the registered array, no two registrations
+// share a page, and the span unregistered is exactly the span registered.
+constexpr uintptr_t kHostPage = 4096;
+struct HostRegion {
+    size_t bytes = 0;       // the caller's range [base, base + bytes)
+    uintptr_t lo = 0, hi = 0;  // page-locked span [lo, hi), page-aligned, inside the caller's range; empty: nothing locked
+};
+// The part of a host range that can be DMA'd in place: [lo, hi) inside [p, p + n), page-locked.
+struct HostSpan {
+    const char *p = nullptr;
+    size_t n = 0;
+    uintptr_t lo = 0, hi = 0;
+    bool direct() const { return hi > lo; }
+    size_t head() const { return direct() ? (size_t)(lo - (uintptr_t)p) : n; }   // bytes before the span
+    size_t tail() const { return direct() ? (size_t)((uintptr_t)p + n - hi) : 0; }  // bytes after it
+};
 struct HostRegistry {
     std::mutex mu;
-    std::map<uintptr_t, size_t> regions;  // base -> bytes, disjoint
-    // is [p, p + bytes) inside one registered region?
-    bool covers(const void *p, size_t bytes) {
-        if (!p || !bytes) return false;
+    std::map<uintptr_t, HostRegion> regions;  // caller base -> region, caller ranges disjoint
+    // [p, p + bytes) inside one registered caller range: its page-locked part (empty span otherwise)
+    HostSpan span(const void *p, size_t bytes) {
+        HostSpan s;
+        s.p = static_cast<const char *>(p);
+        s.n = bytes;
+        if (!p || !bytes) return s;
         const uintptr_t a = (uintptr_t)p;
         std::lock_guard<std::mutex> lk(mu);
         auto it = regions.upper_bound(a);
-        if (it == regions.begin()) return false;
+        if (it == regions.begin()) return s;
         --it;
-        return a >= it->first && a + bytes <= it->first + it->second;
+        if (a < it->first || a + bytes > it->first + it->second.bytes || it->second.hi <= it->second.lo) return s;
+        s.lo = std::max(a, it->second.lo);
+        s.hi = std::min(a + bytes, it->second.hi);
+        if (s.hi <= s.lo) s.lo = s.hi = 0;
+        return s;
     }
     ~HostRegistry() {
-        for (auto &r : regions) (void)hipHostUnregister((void *)r.first);
+        for (auto &r : regions)
+            if (r.second.hi > r.second.lo) (void)hipHostUnregister((void *)r.second.lo);
     }
 };
 
+// Does the HIP runtime map host address p as page-locked memory?  (hipPointerGetAttributes: registered
+// and pinned host memory report hipMemoryTypeHost; pageable memory an error or hipMemoryTypeUnregistered.)
+bool hip_knows_host(const void *p) {
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // a failed query is the expected answer for pageable memory: clear it
+        return false;
+    }
+    return a.type != hipMemoryTypeUnregistered;
+}
+
+// Host <-> device copies of the byte range [off, off + len) of a caller range whose page-locked part is `s`:
+// the page-locked part straight from / to the caller's memory, the head and tail (< 1 page each) from / to
+// `bounce` (pinned: head at bounce[0, 4096), tail at bounce[4096, 8192)).  h2d: dev <- host.
+hipError_t span_copy(const HostSpan &s, char *bounce, size_t off, size_t len, void *dev, bool h2d, hipStream_t st) {
+    const size_t h = s.head(), t0 = s.n - s.tail();
+    const size_t cut[4] = {0, h, t0, s.n};
+    for (int piece = 0; piece < 3; ++piece) {
+        const size_t b0 = std::max(off, cut[piece]), b1 = std::min(off + len, cut[piece + 1]);
+        if (b1 <= b0) continue;
+        char *host = piece == 1 ? const_cast<char *>(s.p) + b0
+                                : bounce + (piece == 0 ? b0 : kHostPage + (b0 - t0));
+        char *d = static_cast<char *>(dev) + (b0 - off);
+        const hipError_t e = h2d ? hipMemcpyAsync(d, host, b1 - b0, hipMemcpyHostToDevice, st)
+                                 : hipMemcpyAsync(host, d, b1 - b0, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 struct Session {
     int device_index = 0;
+    int64_t id = 0;  // gpu_session_id: distinct for every session opened in the process
     std::vector<std::unique_ptr<DeviceCtx>> devs;
     std::mutex live_mu;
     std::vector<std::unique_ptr<LiveCtx>> live_free;
@@ -744,6 +809,9 @@ struct Batch {
     void *h_in = nullptr, *h_out = nullptr;  // pinned staging (null when the caller's buffer is registered)
     size_t h_in_bytes = 0, h_out_bytes = 0;
     double *direct_out = nullptr;            // registered caller output receiving the D2H copies
+    HostSpan in_span, out_span;              // page-locked parts of the caller's series / output (direct paths)
+    char *bounce = nullptr;                  // pinned: series head / tail [0, 8 KiB), output head / tail [8, 16 KiB)
+    static constexpr size_t kBounce = 4 * kHostPage;
     int status = MTB_OK;
     std::string error;
     ~Batch() {
@@ -758,6 +826,7 @@ struct Batch {
         }
         host_free(h_in, h_in_bytes);
         host_free(h_out, h_out_bytes);
+        host_free(bounce, kBounce);
     }
 };
 
@@ -820,8 +889,18 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
     const size_t es = c.elem();
     const int64_t in_elems = c.series_elems();
     const size_t in_bytes = (size_t)in_elems * es, out_bytes = (size_t)(c.n_windows * c.record()) * es;
-    const bool din = !c.f32 && S.host_regs.covers(series, in_bytes);
-    if (!c.f32 && out_direct && S.host_regs.covers(out_direct, out_bytes)) b->direct_out = out_direct;
+    if (!c.f32) b->in_span = S.host_regs.span(series, in_bytes);
+    if (!c.f32 && out_direct) b->out_span = S.host_regs.span(out_direct, out_bytes);
+    const bool din = b->in_span.direct();
+    if (b->out_span.direct()) b->direct_out = out_direct;
+    if (din || b->direct_out) {  // the < 1-page head / tail of a registered caller range go through here
+        if (!(b->bounce = static_cast<char *>(host_alloc(Batch::kBounce)))) return MTB_NO_MEM;
+        if (din) {
+            const HostSpan &s = b->in_span;
+            memcpy(b->bounce, s.p, s.head());
+            memcpy(b->bounce + kHostPage, s.p + s.n - s.tail(), s.tail());
+        }
+    }
     if (!din) {
         b->h_in_bytes = in_bytes;
         if (!(b->h_in = host_alloc(in_bytes))) return MTB_NO_MEM;
@@ -864,13 +943,24 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
                 stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
                 staged = e1;
             }
-            const char *src = din ? (const char *)(series + e0) : (const char *)b->h_in + (size_t)e0 * es;
-            HIP_OR(hipMemcpyAsync(P.d_in, src, P.in_bytes, hipMemcpyHostToDevice, P.stream), MTB_INTERNAL_ERROR);
+            if (din) {
+                HIP_OR(span_copy(b->in_span, b->bounce, (size_t)e0 * es, P.in_bytes, P.d_in, true, P.stream),
+                       MTB_INTERNAL_ERROR);
+            } else {
+                HIP_OR(hipMemcpyAsync(P.d_in, (const char *)b->h_in + (size_t)e0 * es, P.in_bytes, hipMemcpyHostToDevice,
+                                      P.stream),
+                       MTB_INTERNAL_ERROR);
+            }
             int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
             if (st != MTB_OK) return st;
-            char *dst = b->direct_out ? (char *)(b->direct_out + P.w0 * c.record())
-                                      : (char *)b->h_out + (size_t)(P.w0 * c.record()) * es;
-            HIP_OR(hipMemcpyAsync(dst, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream), MTB_INTERNAL_ERROR);
+            const size_t o0 = (size_t)(P.w0 * c.record()) * es;
+            if (b->direct_out) {
+                HIP_OR(span_copy(b->out_span, b->bounce + 2 * kHostPage, o0, P.out_bytes, P.d_out, false, P.stream),
+                       MTB_INTERNAL_ERROR);
+            } else {
+                HIP_OR(hipMemcpyAsync((char *)b->h_out + o0, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream),
+                       MTB_INTERNAL_ERROR);
+            }
             HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
             P.recorded = true;
         }
@@ -915,6 +1005,12 @@ int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int3
         const int64_t r1 = std::min<int64_t>(p.w0 + p.nw, nrec);
         stage_out(out + p.w0 * rec, (const char *)b.h_out + (size_t)(p.w0 * rec) * b.cfg.elem(), (r1 - p.w0) * rec,
                   b.cfg.f32);
+    }
+    if (b.direct_out && wait) {  // every part done: the head / tail of the caller's array from the bounce buffer
+        const HostSpan &s = b.out_span;
+        char *o = reinterpret_cast<char *>(b.direct_out);
+        memcpy(o, b.bounce + 2 * kHostPage, s.head());
+        memcpy(o + s.n - s.tail(), b.bounce + 3 * kHostPage, s.tail());
     }
     *n_out = (int32_t)nrec;
     return MTB_OK;
@@ -1310,6 +1406,8 @@ MTB_API int32_t gpu_init(int32_t device_index, int32_t stream_count) {
             D.streams.push_back(st);
         }
     }
+    static int64_t next_id = 0;  // under g_session_mu
+    S->id = ++next_id;
     g_session = S;
     g_session_refs = 1;
     g_thread_refs->clear();
@@ -1360,22 +1458,52 @@ MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
     }
     const uintptr_t a = (uintptr_t)ptr;
     const size_t bytes = (size_t)count * sizeof(double);
+    if (a + bytes < a) {
+        set_error("gpu_register_host: [%p, +%zu B) wraps the address space", (const void *)ptr, bytes);
+        return MTB_BAD_ARGS;
+    }
     HostRegistry &R = S->host_regs;
     std::lock_guard<std::mutex> lk(R.mu);
+    // caller ranges are disjoint (so are the page-locked spans inside them: no page is locked twice)
     auto it = R.regions.lower_bound(a);
     const bool overlaps = (it != R.regions.end() && it->first < a + bytes) ||
-                          (it != R.regions.begin() && std::prev(it)->first + std::prev(it)->second > a);
+                          (it != R.regions.begin() && std::prev(it)->first + std::prev(it)->second.bytes > a);
     if (overlaps) {
         set_error("gpu_register_host: [%p, +%zu B) overlaps a registered buffer", (const void *)ptr, bytes);
         return MTB_BAD_ARGS;
     }
-    const hipError_t e = hipHostRegister(const_cast<double *>(ptr), bytes, hipHostRegisterPortable);
-    if (e != hipSuccess) {
-        set_error("hipHostRegister(%zu bytes): %s", bytes, hipGetErrorString(e));
-        return MTB_INTERNAL_ERROR;
+    HostRegion r;
+    r.bytes = bytes;
+    r.lo = (a + kHostPage - 1) & ~(kHostPage - 1);
+    r.hi = (a + bytes) & ~(kHostPage - 1);
+    if (r.hi <= r.lo) {
+        r.lo = r.hi = 0;  // no whole page inside the buffer: nothing to lock, batches stage it (still registered)
+    } else {
+        if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
+            set_error("gpu_register_host: [%p, +%zu B) is already page-locked (hipHostMalloc / another registration)",
+                      (const void *)ptr, bytes);
+            return MTB_BAD_ARGS;
+        }
+        const hipError_t e = hipHostRegister((void *)r.lo, r.hi - r.lo, hipHostRegisterPortable);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipHostRegister(%p, %zu bytes): %s", (void *)r.lo, (size_t)(r.hi - r.lo), hipGetErrorString(e));
+            return MTB_INTERNAL_ERROR;
+        }
+        if (!hip_knows_host((const void *)r.lo) || !hip_knows_host((const void *)(r.hi - 1))) {
+            (void)hipHostUnregister((void *)r.lo);
+            set_error("gpu_register_host: HIP does not report [%p, %p) as page-locked after hipHostRegister",
+                      (void *)r.lo, (void *)r.hi);
+            return MTB_INTERNAL_ERROR;
+        }
     }
-    R.regions.emplace(a, bytes);
+    R.regions.emplace(a, r);
     return MTB_OK;
+}
+
+MTB_API int64_t gpu_session_id(void) {
+    auto S = session();
+    return S ? S->id : 0;
 }
 
 MTB_API int32_t gpu_unregister_host(const double *ptr) {
@@ -1391,12 +1519,22 @@ MTB_API int32_t gpu_unregister_host(const double *ptr) {
         set_error("gpu_unregister_host: %p is not the start of a registered buffer", (const void *)ptr);
         return MTB_BAD_ARGS;
     }
-    const hipError_t e = hipHostUnregister(const_cast<double *>(ptr));
-    R.regions.erase(it);
-    if (e != hipSuccess) {
-        set_error("hipHostUnregister: %s", hipGetErrorString(e));
-        return MTB_INTERNAL_ERROR;
+    const HostRegion r = it->second;
+    if (r.hi > r.lo) {
+        const hipError_t e = hipHostUnregister((void *)r.lo);
+        if (e != hipSuccess) {  // the range stays registered (and in the table): the caller must not free it
+            (void)hipGetLastError();
+            set_error("hipHostUnregister(%p): %s; the buffer is still page-locked", (void *)r.lo, hipGetErrorString(e));
+            return MTB_INTERNAL_ERROR;
+        }
+        R.regions.erase(it);
+        if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
+            set_error("gpu_unregister_host: HIP still maps [%p, %p) after hipHostUnregister", (void *)r.lo, (void *)r.hi);
+            return MTB_INTERNAL_ERROR;
+        }
+        return MTB_OK;
     }
+    R.regions.erase(it);
     return MTB_OK;
 }
 
@@ -1852,7 +1990,7 @@ MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
     constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..7", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..8", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "gpu_set_kalman_params": (C.c_int32, [_d, C.c_int32]),
     "gpu_register_host": (C.c_int32, [_d, C.c_int64]),
     "gpu_unregister_host": (C.c_int32, [_d]),
+    "gpu_session_id": (C.c_int64, []),
     "gpu_spectrum_topk_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                             C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32, _i32p]),
     "wsp_plan_set_topk": (C.c_int32, [C.c_int64, C.c_int32, C.c_double, C.c_double]),
@@ -271,7 +272,14 @@ def register_host(a: np.ndarray) -> None:
 
 
 def unregister_host(a: np.ndarray) -> None:
+    """gpu_unregister_host: raises on every failure -- an unknown buffer (BAD_ARGS) and a runtime that
+    refused or still maps the range (INTERNAL_ERROR: the buffer stays page-locked and must not be freed)."""
     _check("gpu_unregister_host", lib().gpu_unregister_host(_dptr(a)))
+
+
+def session_id() -> int:
+    """gpu_session_id: > 0 for the open session (changes when a new session is opened), 0 without one."""
+    return int(lib().gpu_session_id())
 
 
 def set_kalman_params(params) -> None:

@@ -50,6 +50,7 @@ class FeedCache:
     from_file: bool = False
     chrono: np.ndarray = field(default_factory=lambda: np.empty(0))
     pinned: bool = False
+    pinned_session: int = 0  # gpu_session_id of the session holding the registration
 
 
 def save_feed_cache(path: str, close_newest_first: np.ndarray) -> None:
@@ -130,26 +131,29 @@ def _restage(cache: FeedCache) -> None:
 def pin_feed_cache(cache: FeedCache) -> None:
     """Page-lock the feed history for the device (gpu_register_host, needs an open session):
     synchronous batch calls on ``cache.chrono`` then DMA it in place instead of copying it
-    through the library's staging buffers (include/mtbridge.h, "Pinned feed staging")."""
+    through the library's staging buffers (include/mtbridge.h, "Pinned feed staging").  The
+    session that holds the registration is remembered (gpu_session_id)."""
     if cache.chrono.size != cache.close.size:
         cache.chrono = np.ascontiguousarray(cache.close[::-1], dtype=np.float64)
     if cache.chrono.size and not cache.pinned:
         bridge.register_host(cache.chrono)
         cache.pinned = True
+        cache.pinned_session = bridge.session_id()
 
 
 def unpin_feed_cache(cache: FeedCache) -> None:
-    """gpu_unregister_host of the pinned history.  A registration belongs to the session: once the
-    last gpu_shutdown has torn the session down (FftProcessor.shutdown in on_calculate may be that
-    call) the library no longer holds it -- the pages were unlocked with the session -- so an
-    unknown buffer or a missing session leaves nothing to undo and only clears the flag."""
-    if cache.pinned:
-        cache.pinned = False
-        try:
-            bridge.unregister_host(cache.chrono)
-        except bridge.BridgeError as e:
-            if e.status not in (bridge.BAD_ARGS, bridge.BACKEND_UNAVAILABLE):
-                raise
+    """gpu_unregister_host of the pinned history.  A registration belongs to the session that made it:
+    once the last gpu_shutdown has torn that session down (FftProcessor.shutdown in on_calculate may be
+    that call) the pages were unlocked with it, so there is nothing to undo -- the session id tells.
+    Under the same session every failure is raised: an unregistration that did not happen leaves the
+    buffer page-locked, and freeing it then is what the round-4 faults were made of."""
+    if not cache.pinned:
+        return
+    if bridge.session_id() != cache.pinned_session:
+        cache.pinned = False  # the session that held it is gone: its registrations went with it
+        return
+    bridge.unregister_host(cache.chrono)
+    cache.pinned = False
 
 
 class FeedBuilder:

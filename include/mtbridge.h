@@ -239,12 +239,31 @@ MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
  * convert and truncated outputs (out_cap below all records) still stage;
  * gpu_submit_spectrum_batch still copies its input (1.1.0:1316).
  * Registrations belong to the session and end with it (last gpu_shutdown).
- * The caller must not unregister or free a buffer while a call reading it
- * runs.  MTB_OK; MTB_BAD_ARGS for null/empty or overlapping ranges (register)
- * or an unknown base pointer (unregister); MTB_BACKEND_UNAVAILABLE without a
- * session; MTB_INTERNAL_ERROR when the runtime refuses. */
+ *
+ * Page granularity (round 5): only the whole pages INSIDE [ptr, ptr + count)
+ * are page-locked -- the page-exact span [round_up(ptr, 4096),
+ * round_down(ptr + count, 4096)) -- never a page the buffer shares with other
+ * memory; the < 1-page head and tail of the buffer go through a small pinned
+ * bounce buffer of each call.  A buffer with no whole page inside is
+ * registered without locking anything (its calls stage).  After
+ * hipHostRegister / hipHostUnregister the library checks with
+ * hipPointerGetAttributes that the runtime maps / no longer maps the span.
+ *
+ * The caller must not free, move (ArrayResize) or unregister a buffer while
+ * it is registered and a call reading it runs, and must unregister it before
+ * freeing it.  MTB_OK; MTB_BAD_ARGS for null/empty ranges, ranges overlapping
+ * another registration or already page-locked memory (register) or an unknown
+ * base pointer (unregister); MTB_BACKEND_UNAVAILABLE without a session;
+ * MTB_INTERNAL_ERROR when the runtime refuses, or when after unregistering it
+ * still maps the span -- a failed hipHostUnregister leaves the registration in
+ * place (the buffer stays locked and must not be freed). */
 MTB_API int32_t gpu_register_host(const double *ptr, int64_t count);
 MTB_API int32_t gpu_unregister_host(const double *ptr);
+/* The current session's identity: a number > 0 that changes whenever the
+ * session is torn down (last gpu_shutdown) and a new one opened; 0 without a
+ * session.  Registrations belong to one session: a caller that registered a
+ * buffer under session id s and finds another id has nothing to unregister. */
+MTB_API int64_t gpu_session_id(void);
 
 /* =====================================================================
  * 4. Device-resident plans: the same hot path on buffers already in HBM
@@ -298,7 +317,7 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
-/* Tuning / ablation: the kernel form, 0..7 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -306,7 +325,8 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    probe-threshold scan (16 windows per batch, 4 waves per SIMD), 4 / 5 = the
  *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
- *    windows; 2 = the same pipelined over two internal streams; 3 = the fused
+ *    windows; 2 = the same pipelined over two internal streams (a one-window
+ *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused
  *    one-workgroup-per-window kernel (N = 65536 / 131072; the default for fp64
  *    N = 65536); 4 = its 256-thread form with register prefetch; 5 = the fused
  *    kernel with plain (not non-temporal) output stores; 6 = fp64 N = 262144

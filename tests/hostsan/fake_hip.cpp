@@ -110,6 +110,30 @@ int dev_of(const void *p) {  // -1: not device memory (host, pinned or registere
     --it;
     return a < it->first + it->second.first ? it->second.second : -1;
 }
+// page-locked host ranges: base -> bytes (hipHostRegister)
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_regs;
+std::atomic<int64_t> g_direct{0};
+bool reg_covers(const void *p, size_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.upper_bound(a);
+    if (it == g_regs.begin()) return false;
+    --it;
+    return a >= it->first && a + n <= it->first + it->second;
+}
+// hipHostMalloc'd blocks: base -> bytes
+std::mutex g_pinned_mu;
+std::map<uintptr_t, size_t> g_pinned;
+bool host_locked(const void *p) {
+    if (reg_covers(p, 1)) return true;
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a < it->first + it->second;
+}
 constexpr int kMaxDev = 64;
 std::atomic<int64_t> g_windows[kMaxDev];
 std::atomic<int64_t> g_violations{0};
@@ -162,14 +186,65 @@ hipError_t hipFree(void *p) {
 }
 hipError_t hipHostMalloc(void **p, size_t n, unsigned int) {
     *p = aligned_alloc(256, (n + 255) & ~size_t(255));
-    return *p ? hipSuccess : hipErrorOutOfMemory;
+    if (!*p) return hipErrorOutOfMemory;
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    g_pinned[(uintptr_t)*p] = n ? n : 1;
+    return hipSuccess;
 }
 hipError_t hipHostFree(void *p) {
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned.erase((uintptr_t)p);
+    }
     free(p);
     return hipSuccess;
 }
-hipError_t hipHostRegister(void *, size_t, unsigned int) { return hipSuccess; }
-hipError_t hipHostUnregister(void *) { return hipSuccess; }
+// Page-locked host ranges (hipHostRegister).  The library must register whole pages only (round 5: the
+// page-exact span inside the caller's buffer): a range that is not page-aligned at both ends,
+// or that shares a page with a live registration, counts as a violation and is refused.  Copies whose host
+// side lies in a registered range count as direct (fakehip_direct_copies).
+hipError_t hipHostRegister(void *p, size_t n, unsigned int) {
+    const uintptr_t a = (uintptr_t)p;
+    if (!p || !n || a % 4096 || n % 4096) {
+        g_violations++;
+        return hipErrorInvalidValue;
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.lower_bound(a);
+    if ((it != g_regs.end() && it->first < a + n) || (it != g_regs.begin() && std::prev(it)->first + std::prev(it)->second > a)) {
+        g_violations++;
+        return hipErrorHostMemoryAlreadyRegistered;
+    }
+    g_regs[a] = n;
+    return hipSuccess;
+}
+hipError_t hipHostUnregister(void *p) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.find((uintptr_t)p);
+    if (it == g_regs.end()) return hipErrorHostMemoryNotRegistered;
+    g_regs.erase(it);
+    return hipSuccess;
+}
+// registered / pinned host memory: hipMemoryTypeHost; device memory: hipMemoryTypeDevice; anything else
+// (pageable memory) an error, as the real runtime answers (scripts/hostreg_probe.py)
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t *attr, const void *p) {
+    memset(attr, 0, sizeof(*attr));
+    if (host_locked(p)) {
+        attr->type = hipMemoryTypeHost;
+        attr->hostPointer = const_cast<void *>(p);
+        attr->devicePointer = const_cast<void *>(p);
+        return hipSuccess;
+    }
+    const int d = dev_of(p);
+    if (d >= 0) {
+        attr->type = hipMemoryTypeDevice;
+        attr->device = d;
+        attr->devicePointer = const_cast<void *>(p);
+        return hipSuccess;
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t hipGetLastError(void) { return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int) {
     *d = h;
     return hipSuccess;
@@ -182,8 +257,10 @@ hipError_t hipMemset(void *d, int v, size_t n) {
     memset(d, v, n);
     return hipSuccess;
 }
-hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t st) {
+hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st) {
     check_op(st, {d, s});
+    const void *host = k == hipMemcpyHostToDevice ? s : (k == hipMemcpyDeviceToHost ? d : nullptr);
+    if (host && reg_covers(host, n)) g_direct++;
     run_on(st, [=] { memcpy(d, s, n); });
     return hipSuccess;
 }
@@ -269,6 +346,11 @@ void fakehip_reset(void) {
 }
 int64_t fakehip_windows(int dev) { return dev >= 0 && dev < kMaxDev ? g_windows[dev].load() : -1; }
 int64_t fakehip_violations(void) { return g_violations.load(); }
+int64_t fakehip_direct_copies(void) { return g_direct.load(); }
+int64_t fakehip_registered_ranges(void) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    return (int64_t)g_regs.size();
+}
 }  // extern "C"
 
 // ---- kernel launch stubs (wsp_internal.h): record element k of window w = x_w[k % N] + k

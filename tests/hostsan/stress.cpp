@@ -14,7 +14,9 @@
 //     two threads while a third toggles the mode / segment and destroys them;
 //   * pinned feeds (gpu_register_host): threads registering their series and
 //     output arrays, running synchronous batches through them, unregistering,
-//     and two threads racing to register overlapping ranges of one buffer.
+//     and two threads racing to register overlapping ranges of one buffer;
+//     buffers that neither start nor end on a page (only their whole inner
+//     pages may be page-locked, the head / tail go through the bounce buffer).
 // Every record is checked against the fake kernels' formula
 // (record element k of window w = x[w*hop + k % N] + k).  Exit 0 = all good.
 #include <dlfcn.h>
@@ -226,6 +228,47 @@ void pinned_feed(int sym) {  // FeedCache rewired to pinned buffers, one chart's
     A.shutdown();
 }
 
+// registered ranges that do not start or end on a page: the library locks only the whole pages inside them
+// (the fake runtime refuses anything else and counts it as a violation), DMAs those in place and routes the
+// head / tail through its bounce buffer -- every record must still land, and the in-place copies must happen
+int64_t (*g_direct_copies)(void) = nullptr;
+int64_t (*g_violations)(void) = nullptr;
+int64_t (*g_registered)(void) = nullptr;
+void pinned_edges(int sym) {
+    CHECK(A.init(0, 16) == MTB_OK, "init edges %d", sym);
+    const int n = 256, hop = 1 + sym, len = 5000 + 37 * sym;
+    std::vector<double> sbuf(len + 1024), obuf;
+    const std::vector<double> s0 = series_of(80 + sym, len);
+    double *s = sbuf.data() + 3 + 61 * sym;  // not page-aligned, several pages long
+    std::copy(s0.begin(), s0.end(), s);
+    const int nwin = 1 + (len - n) / hop, rec = n / 2;
+    obuf.resize((size_t)nwin * rec + 1024);
+    double *out = obuf.data() + 5 + 13 * sym;
+    for (int r = 0; r < 10; ++r) {
+        const int64_t d0 = g_direct_copies();
+        CHECK(A.reg(s, len) == MTB_OK && A.reg(out, (int64_t)nwin * rec) == MTB_OK, "register edges %d", sym);
+        std::fill(out, out + (size_t)nwin * rec, -1.0);
+        int got = 0;
+        CHECK(A.batch(s, len, n, hop, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, out,
+                      nwin * rec, &got) == MTB_OK && got == nwin, "edges batch %d", sym);
+        CHECK(check_records(s0, out, n, hop, nwin, rec), "edges records %d round %d", sym, r);
+        CHECK(g_direct_copies() > d0, "edges: no in-place DMA %d", sym);
+        CHECK(A.unreg(out) == MTB_OK && A.unreg(s) == MTB_OK, "unregister edges %d", sym);
+    }
+    // a buffer with no whole page inside: registered (nothing locked), its batches stage
+    std::vector<double> tiny(400);
+    const std::vector<double> t0 = series_of(90 + sym, 300);
+    std::copy(t0.begin(), t0.end(), tiny.begin() + 1);
+    CHECK(A.reg(tiny.data() + 1, 300) == MTB_OK, "register tiny %d", sym);
+    std::vector<double> tout(45 * 32);
+    int got = 0;
+    CHECK(A.batch(tiny.data() + 1, 300, 64, 5, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER,
+                  tout.data(), (int)tout.size(), &got) == MTB_OK && got == 48 - 3, "tiny batch %d", sym);
+    CHECK(check_records(t0, tout.data(), 64, 5, got, 32), "tiny records %d", sym);
+    CHECK(A.unreg(tiny.data() + 1) == MTB_OK, "unregister tiny %d", sym);
+    A.shutdown();
+}
+
 void register_race() {  // two threads register overlapping ranges of one buffer: exactly one wins
     CHECK(A.init(0, 16) == MTB_OK, "init race");
     std::vector<double> buf(1 << 16);
@@ -267,6 +310,9 @@ int main(int argc, char **argv) {
     sym(h, A.group_set_mode, "wsp_group_set_mode");
     sym(h, A.group_set_segment, "wsp_group_set_segment");
     sym(h, A.group_destroy, "wsp_group_destroy");
+    sym(h, g_direct_copies, "fakehip_direct_copies");
+    sym(h, g_violations, "fakehip_violations");
+    sym(h, g_registered, "fakehip_registered_ranges");
     for (int m = 0; m < 5; ++m) {
         g_gin.push_back(series_of(60 + m, (int)kGWins[m] + kGLens[m] - 1));
         for (int k = 0; k < 2; ++k) g_gout[k].emplace_back((size_t)kGWins[m] * (kGLens[m] / 2));
@@ -281,6 +327,7 @@ int main(int argc, char **argv) {
     th.emplace_back(free_race);
     th.emplace_back(plan_race);
     for (int c = 0; c < 4; ++c) th.emplace_back(pinned_feed, c);
+    for (int c = 0; c < 3; ++c) th.emplace_back(pinned_edges, c);
     th.emplace_back(register_race);
     th.emplace_back(group_race);
     for (auto &t : th) t.join();
@@ -293,6 +340,9 @@ int main(int argc, char **argv) {
                   (int)out.size(), &got) == MTB_OK && got == 8, "final batch");
     CHECK(check_records(s, out.data(), 128, 128, 8, 64), "final records");
     A.shutdown();
+    CHECK(g_registered() == 0, "page-locked ranges left after the last shutdown: %lld", (long long)g_registered());
+    CHECK(g_violations() == 0, "fake runtime violations (unaligned / overlapping registrations): %lld",
+          (long long)g_violations());
     CHECK(A.init(-1, 4) == MTB_OK, "device switch after the last shutdown");
     A.shutdown();
     printf("hostsan stress: %s (%d failures)\n", g_fail ? "FAIL" : "ok", g_fail.load());

@@ -89,10 +89,13 @@ def test_large_chunks(gpu_session):
     assert oracle.rel_err(p, ref(s, n, 2048, "iir", "hann", 1024)) <= TOL["f64"]
 
 
-@pytest.mark.parametrize("n,chunk", [(262144, 5), (131072, 1), (32768, 100)])
-def test_large_set_chunk(gpu_session, n, chunk):
+@pytest.mark.parametrize("n,chunk,variant", [(262144, 5, 1), (131072, 1, 1), (32768, 100, 1),
+                                             (32768, 1, 2), (32768, 2, 2), (131072, 1, 2)])
+def test_large_set_chunk(gpu_session, n, chunk, variant):
     """wsp_plan_set_chunk: the two-pass path over other chunk lengths (ragged last chunk, one window per chunk)
-    gives the same records as the library's chunking (the same kernels on other chunk boundaries)."""
+    gives the same records as the library's chunking (the same kernels on other chunk boundaries).  Variant 2
+    (the pipelined two-pass form, two Y buffers of chunk / 4 windows) at one and two windows per chunk: a
+    one-window workspace cannot hold its second buffer, so the plan runs the plain chunk loop."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     nwin = 13 if n > 65536 else 211
@@ -101,7 +104,7 @@ def test_large_set_chunk(gpu_session, n, chunk):
     outs = []
     for c in (0, chunk):
         plan = bridge.Plan(0, n, n, nwin, "mean", "hann")
-        plan.set_variant(1)  # the two-pass path
+        plan.set_variant(variant if c else 1)  # the two-pass path (the reference run: variant 1, default chunk)
         plan.set_chunk(c)
         o = torch.empty(nwin * plan.record, dtype=torch.float64, device=dev)
         plan.execute(d_s.data_ptr(), o.data_ptr(), torch.cuda.current_stream().cuda_stream)

@@ -629,3 +629,155 @@ def test_kalman_params(gpu_session, prec, kw):
     s_ref = s.astype(np.float32).astype(np.float64) if prec == "f32" else s
     r = oracle.batch_spectrum(s_ref, n, n, "kalman", "hann", 0, kalman=kp)
     assert oracle.rel_err(p, r) <= TOL[prec], kw
+
+
+def test_register_host_direct_dma(gpu_session):
+    """gpu_register_host: a registered fp64 series is DMA'd in place and a registered output array
+    receives the results directly (no staging copy); results identical to the staged path."""
+    n, hop = 1024, 256
+    s = synth.random_walk(300 * hop + n, seed=41)
+    nwin = 1 + (s.size - n) // hop
+    staged = gpu(s, n, hop, "iir", "hann", 512)
+    out = np.full(nwin * (n // 2), np.nan)
+    bridge.register_host(s)
+    bridge.register_host(out)
+    try:
+        p = bridge.spectrum_batch(s, n, hop, "iir", "hann", 512, out=out)
+        assert p.base is out or p.base is out.base or np.shares_memory(p, out)
+        assert np.array_equal(p, staged)
+        assert oracle.rel_err(p, ref(s, n, hop, "iir", "hann", 512)) <= TOL["f64"]
+        # a view inside the registered series is covered as well (sub-range of the region)
+        sub = s[37 * hop:]
+        assert oracle.rel_err(gpu(sub, n, hop), ref(sub, n, hop)) <= TOL["f64"]
+        # fp32 plans convert and truncated outputs stage: same results as without registration
+        p32 = gpu(s, n, hop, "kalman", "hann", prec="f32")
+        assert oracle.rel_err(p32, ref(s.astype(np.float32).astype(np.float64), n, hop, "kalman", "hann")) <= TOL["f32"]
+        part = bridge.spectrum_batch(s, n, hop, "iir", "hann", 512, max_records=10, out=out)
+        assert np.array_equal(part, staged[:10])
+        # top-k and the legacy batch FFT take the same path
+        tk = bridge.spectrum_topk_batch(s, n, hop)
+        w = s[: 8 * n].reshape(8, n).copy()  # its own buffer (a view of s would overlap s)
+        bridge.register_host(w)
+        fb = bridge.fft_real_forward_batch(w)
+        bridge.unregister_host(w)
+        assert oracle.rel_err(fb, ref(w.reshape(-1), n, n, "none", "none", output="packed")) <= 1e-12
+        assert tk.shape == (nwin, 8, 4)
+        # overlapping and unknown ranges are refused
+        with pytest.raises(bridge.BridgeError) as e:
+            bridge.register_host(s[10:20])
+        assert e.value.status == bridge.BAD_ARGS
+        with pytest.raises(bridge.BridgeError) as e:
+            bridge.unregister_host(s[10:])
+        assert e.value.status == bridge.BAD_ARGS
+    finally:
+        bridge.unregister_host(out)
+        bridge.unregister_host(s)
+    with pytest.raises(bridge.BridgeError):
+        bridge.unregister_host(s)
+
+
+def test_pinned_feed_cache_grows(gpu_session, tmp_path):
+    """FeedCache rewired to pinned buffers: pin_feed_cache registers the chronological history;
+    ensure_feed_cache re-registers it when more bars arrive; feed_spectra runs on it in place."""
+    n = 512
+    hist = synth.random_walk(6000, seed=9)
+    close = hist[::-1].copy()  # newest first, as CopyClose fills an as-series array
+    cache = indicator.FeedCache()
+    ok, _, _ = indicator.ensure_feed_cache(cache, "EURUSD", "M1", 3000, False, "WaveSpecZZ",
+                                           lambda start, cnt: close[start:start + cnt], str(tmp_path))
+    assert ok and cache.chrono.size == 3000
+    indicator.pin_feed_cache(cache)
+    try:
+        assert cache.pinned
+        p = indicator.feed_spectra(cache, n, 64)
+        assert oracle.rel_err(p, ref(cache.chrono, n, 64, "none", "hann")) <= TOL["f64"]
+        ok, delta, _ = indicator.ensure_feed_cache(cache, "EURUSD", "M1", 6000, False, "WaveSpecZZ",
+                                                   lambda start, cnt: close[start:start + cnt], str(tmp_path))
+        assert ok and delta == 3000 and cache.pinned and cache.chrono.size == 6000
+        assert np.array_equal(cache.chrono, hist)
+        p = indicator.feed_spectra(cache, n, 64)
+        assert oracle.rel_err(p, ref(hist, n, 64, "none", "hann")) <= TOL["f64"]
+    finally:
+        indicator.unpin_feed_cache(cache)
+    assert not cache.pinned
+
+
+def _hip_knows(addr: int) -> bool:
+    """hipPointerGetAttributes on a host address (the runtime torch loaded, the library's): page-locked?"""
+    class Attr(C.Structure):
+        _fields_ = [("type", C.c_int), ("device", C.c_int), ("devicePointer", C.c_void_p),
+                    ("hostPointer", C.c_void_p), ("isManaged", C.c_int), ("allocationFlags", C.c_uint)]
+    hip = C.CDLL("libamdhip64.so.7")
+    a = Attr()
+    e = hip.hipPointerGetAttributes(C.byref(a), C.c_void_p(addr))
+    hip.hipGetLastError()
+    return e == 0 and a.type != 0
+
+
+def test_register_host_page_edges(gpu_session):
+    """Round 5: only the whole pages inside a registered buffer are page-locked.
+    Buffers that start and end mid-page, share pages with each other and with unregistered memory, and one
+    with no whole page inside: the batch results equal the staged path's, the runtime maps exactly the inner
+    pages while registered and nothing after unregistering, and a registration over an already registered
+    buffer's pages is refused."""
+    page = 4096
+    n, hop = 512, 7
+    arena = np.zeros((16 << 20) // 8)  # one allocation holding several neighbouring arrays
+    first = ((37 * 8 - arena.ctypes.data % page) % page) // 8 + page // 8  # 37 doubles past a page start
+    s = arena[first:first + 40000]
+    s[:] = synth.random_walk(s.size, seed=43)
+    nwin = 1 + (s.size - n) // hop
+    out = arena[first + 40000:first + 40000 + nwin * (n // 2)]  # starts in s's last page
+    assert out.ctypes.data // page == (s.ctypes.data + s.nbytes - 1) // page
+    staged = gpu(s.copy(), n, hop, "mean", "hann")
+    sid = bridge.session_id()
+    assert sid > 0
+    bridge.register_host(s)
+    bridge.register_host(out)
+    try:
+        lo = -(-s.ctypes.data // page) * page
+        hi = (s.ctypes.data + s.nbytes) // page * page
+        assert _hip_knows(lo) and _hip_knows(hi - 1)
+        assert not _hip_knows(lo - 1) and not _hip_knows(hi)  # the shared head / tail pages stay pageable
+        p = bridge.spectrum_batch(s, n, hop, "mean", "hann", out=out)
+        assert np.shares_memory(p, out) and np.array_equal(p, staged)
+        sub = s[1001:-333]  # a view that starts and ends mid-page inside the registered span
+        assert np.array_equal(gpu(sub, n, hop, "mean", "hann"), gpu(sub.copy(), n, hop, "mean", "hann"))
+        with pytest.raises(bridge.BridgeError) as e:
+            bridge.register_host(s[5:9])
+        assert e.value.status == bridge.BAD_ARGS
+        assert bridge.session_id() == sid
+    finally:
+        bridge.unregister_host(out)
+        bridge.unregister_host(s)
+    assert not _hip_knows(lo) and not _hip_knows(hi - 1)
+    tiny = arena[first + 3:first + 300]  # no whole page inside: registered, nothing locked, batches stage
+    bridge.register_host(tiny)
+    try:
+        assert not _hip_knows(tiny.ctypes.data)
+        assert np.array_equal(gpu(tiny, 64, 5), gpu(tiny.copy(), 64, 5))
+    finally:
+        bridge.unregister_host(tiny)
+
+
+def test_pageable_copies_after_registrations(gpu_session):
+    """The round-4 fault sequence (profiles/r04/faults): numpy arrays registered and unregistered, freed, and
+    then pageable device-to-host and host-to-device copies through torch into freshly allocated host memory
+    of many sizes (the heap then reuses the freed pages) -- every byte must arrive."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    for r in range(6):
+        arrs = [synth.random_walk(m, seed=r * 10 + i) for i, m in enumerate((3000, 8192 + 5, 70001, 300 * 256 + 1024))]
+        for a in arrs:
+            bridge.register_host(a)
+        p = bridge.spectrum_batch(arrs[3], 1024, 256, "none", "hann")
+        for a in arrs:
+            bridge.unregister_host(a)
+        del arrs
+        for m in (1 << 10, 3 << 12, 1 << 17, 5 << 18, 1 << 21):
+            d = torch.arange(m, dtype=torch.float64, device=dev) + r
+            h = d.cpu()
+            assert h[-1].item() == m - 1 + r and h[0].item() == r
+            back = torch.from_numpy(np.full(m, float(r))).to(dev)
+            assert back.sum().item() == r * m
+        assert np.isfinite(p).all()
