@@ -1217,6 +1217,8 @@ struct Group {
     int mode = 0;
     int *ctr = nullptr;                    // 256 task-counter slots (counter, done) on the device, zeroed at create
     uint32_t exec_no = 0;
+    long long *trace = nullptr;            // wsp_group_set_trace: diagnostic per-task timeline of the mixed launch
+    int64_t trace_cap = 0, last_tasks = 0;
     // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;  // [0] fork, [k] join of internal stream k - 1
@@ -1328,6 +1330,8 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
         return MTB_BAD_ARGS;
     }
     m.n_tasks = (int)tasks;
+    g.last_tasks = tasks;
+    m.trace = g.trace && tasks <= g.trace_cap ? g.trace : nullptr;
     const int slot = (int)(g.exec_no++ % kMixSlots);
     m.counter = g.ctr + 2 * slot;
     m.done = g.ctr + 2 * slot + 1;
@@ -2239,6 +2243,25 @@ MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::lock_guard<std::mutex> lk(g->mu);
     g->mode = mode;
     return MTB_OK;
+}
+
+MTB_API int32_t wsp_group_set_trace(int64_t group, void *d_trace, int64_t capacity_tasks) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g || capacity_tasks < 0 || (capacity_tasks > 0 && !d_trace)) {
+        set_error("wsp_group_set_trace(%lld): unknown group or null buffer", (long long)group);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->trace = capacity_tasks ? static_cast<long long *>(d_trace) : nullptr;
+    g->trace_cap = capacity_tasks;
+    return MTB_OK;
+}
+
+MTB_API int64_t wsp_group_last_tasks(int64_t group) {
+    std::shared_ptr<Group> g = find_group(group);
+    if (!g) return -1;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return g->last_tasks;
 }
 
 MTB_API int32_t wsp_group_destroy(int64_t group) {

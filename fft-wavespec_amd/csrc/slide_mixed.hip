@@ -100,7 +100,7 @@ __device__ __forceinline__ bool mix_seg(MixP m, int c, int64_t s, const void *&s
 }
 
 template <typename T, int LOG2N, int NF, int DETREND, int BS>
-__device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq) {
+__device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq, long long *trace) {
     // BS: bins per thread for N <= 1024 (2 by default, the per-length launches' geometry: 0.737 against 0.777 ms
     // for C5 at 4, which holds 4 / 8 segments side by side; profiles/r04/ab).  One-wave 512-point sub-workgroups
     // with wave fences instead of lockstep barriers lost too (0.812 against 0.735 ms: the N = 512 tail then has
@@ -167,6 +167,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
         if (DETREND == kDetrendMean && mm == 0) sum = buf[0].x;  // sum of x - L
         __syncthreads();
     }
+    if (trace && threadIdx.x == 0) trace[2] = wall_clock64();  // diagnostic timeline: seeds done
 #pragma unroll
     for (int b = 0; b < B; ++b)
 #pragma unroll
@@ -237,12 +238,20 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
         for (int i = 1; i < kMixClass; ++i)
             if (c == i) t0 = m->task0[i], l2 = m->log2n[i];
         const int64_t local = task - t0;
-        switch (l2) {
-        case 12: mix_task<T, 12, NF, DETREND, BS>(m, c, local, lds, twq); break;
-        case 11: mix_task<T, 11, NF, DETREND, BS>(m, c, local, lds, twq); break;
-        case 10: mix_task<T, 10, NF, DETREND, BS>(m, c, local, lds, twq); break;
-        default: mix_task<T, 9, NF, DETREND, BS>(m, c, local, lds, twq); break;
+        long long *tr = m->trace ? m->trace + 4 * (int64_t)task : nullptr;  // diagnostic timeline, off by default
+        if (tr && tid == 0) {
+            unsigned xcc = 0;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            tr[0] = (long long)blockIdx.x | ((long long)(xcc & 15) << 32);
+            tr[1] = wall_clock64();
         }
+        switch (l2) {
+        case 12: mix_task<T, 12, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
+        case 11: mix_task<T, 11, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
+        case 10: mix_task<T, 10, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
+        default: mix_task<T, 9, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
+        }
+        if (tr && tid == 0) tr[3] = wall_clock64();
     }
     if (tid == 0) {  // the last workgroup out resets this execute's counter slot
         __threadfence();

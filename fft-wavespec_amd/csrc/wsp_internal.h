@@ -171,6 +171,8 @@ struct SlideMix {
     const void *omega[kMixClass];       // slide table of class c (SlideArgs::omega)
     const void *tw4096;                 // W_4096^k, double complex: the quarter table of every length
     int *counter, *done;                // this execute's task counter slot (zero on entry, reset by the last workgroup)
+    long long *trace;                   // diagnostic timeline (wsp_group_set_trace), null = off: per task
+                                        // [wg | xcc << 32, start, seeds done, end] in wall-clock ticks (100 MHz)
     int64_t sg0[kMixMax];               // member i: its first segment within its class
     int64_t n_windows[kMixMax];
     const void *series[kMixMax];

@@ -86,6 +86,8 @@ SIGNATURES = {
     "wsp_group_set_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_group_set_mode": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_group_destroy": (C.c_int32, [C.c_int64]),
+    "wsp_group_set_trace": (C.c_int32, [C.c_int64, C.c_void_p, C.c_int64]),
+    "wsp_group_last_tasks": (C.c_int64, [C.c_int64]),
     "wsp_version": (C.c_char_p, []),
 }
 
@@ -404,6 +406,14 @@ class Group:
         N <= 1024 / half-length segments for the shortest window length at every batch size / never) --
         wsp_group_set_mode 0..4, include/mtbridge.h."""
         _check("wsp_group_set_mode", lib().wsp_group_set_mode(self.handle, self.MODES[mode]))
+
+    def set_trace(self, d_trace: int, capacity_tasks: int) -> None:
+        """Diagnostic: per-task timeline of the mixed launch into a device buffer of 4 x capacity int64."""
+        _check("wsp_group_set_trace", lib().wsp_group_set_trace(self.handle, C.c_void_p(d_trace), capacity_tasks))
+
+    @property
+    def last_tasks(self) -> int:
+        return int(lib().wsp_group_last_tasks(self.handle))
 
     def execute(self, d_series, d_out, stream: int = 0) -> None:
         """d_series / d_out: device pointers (ints), one per member."""

@@ -415,6 +415,16 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * with one segment length for every window length (ablation).  MTB_BAD_ARGS
  * outside 0..4. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
+/* Diagnostic: a per-task timeline of the mixed-length launch.  d_trace = a
+ * device buffer of 4 x capacity_tasks int64: task t of each later execute
+ * writes [workgroup | XCC << 32, start, seeds done, end] (wall-clock ticks,
+ * 100 MHz) at 4 t when the execute has at most capacity_tasks tasks.
+ * capacity_tasks = 0 turns it off (the default).  MTB_BAD_ARGS for an unknown
+ * group or a null buffer. */
+MTB_API int32_t wsp_group_set_trace(int64_t group, void *d_trace, int64_t capacity_tasks);
+/* Tasks of the group's last mixed-length execute (0 before the first, -1 for
+ * an unknown group). */
+MTB_API int64_t wsp_group_last_tasks(int64_t group);
 MTB_API int32_t wsp_group_destroy(int64_t group);
 
 MTB_API int32_t wsp_plan_destroy(int64_t plan);

@@ -11,6 +11,7 @@
 #   smoke                    __graft_entry__.smoke()
 #   bench=<cfg>[,<args>]     python bench.py --config <cfg> --steps 100 --warmup 20 --no-cpu-baseline <args>
 #                            (args comma-separated), line bench_<cfg>.json
+#   benchc=<cfg>[,<args>]    the same with the CPU baseline (1 core + the job's cores) in the line
 #   default                  python bench.py (the driver's default line, CPU baseline included)
 #   prof=<cfg>[,<algo>[,<variant>[,<key suffix>[,<extra bench args, + for spaces>]]]]
 #                            rocprofv3 kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own
@@ -60,14 +61,17 @@ for step in "$@"; do
         run 120 $O/smoke.log $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
         cat $O/smoke.log
         ;;
-    bench)
+    bench|benchc)
+        # benchc: the same line with the CPU baseline beside it (1 core + the job's cores, the closing check)
+        cpuflag="--no-cpu-baseline"
+        [ "$key" = "benchc" ] && cpuflag=""
         cfg=${val%%,*}
         extra=""
         [ "$cfg" != "$val" ] && extra=${val#*,}
         # one file per (config, arguments): repeated A/B steps do not overwrite each other
         tagx=$(echo "${extra//,/_}" | tr -c 'A-Za-z0-9_.\n-' '_')
         bf=$O/bench_$cfg${tagx:+_$tagx}
-        run 300 $bf.json $bf.err python bench.py --config $cfg --steps 100 --warmup 20 --no-cpu-baseline ${extra//,/ }
+        run 300 $bf.json $bf.err python bench.py --config $cfg --steps 100 --warmup 20 $cpuflag ${extra//,/ }
         python3 -c "
 import json; d=json.loads(open('$bf.json').read().strip().splitlines()[-1])
 print('$cfg', '$extra', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step'], '%.4g win/s'%d['value'], 'frac %.3f'%d['roofline']['frac'])"

@@ -458,14 +458,27 @@ def test_topk_phase_split_form(gpu_session, n, k, minp, maxp, window):
     winner and its neighbours) against the AoS form (wsp_plan_set_variant 1: every thread's phase chunk) -- the
     same bins and powers to 1e-12 -- and both against the oracle (phases and delays to 1e-8).  Bands whose bins
     0 .. kmax + 1 take 2 / 4 / 8 / 16 bins per lane, and one beyond the split slot (periods 3-300: the AoS form)."""
+    _topk_phase_forms(n, k, minp, maxp, window, n)
+
+
+@pytest.mark.parametrize("n,window", [(4096, "hann"), (2048, "blackman")])
+@pytest.mark.parametrize("hop_of", ["1", "37", "n/4", "n+5"])
+def test_topk_phase_split_form_hops(gpu_session, n, window, hop_of):
+    """the split form reads its samples through a buffer descriptor with unaligned 16-B loads for odd
+    and overlapping hops; hop = 1, an odd hop (37), N/4 and a gap (N + 5) against the AoS form and the oracle."""
+    hop = {"1": 1, "37": 37, "n/4": n // 4, "n+5": n + 5}[hop_of]
+    _topk_phase_forms(n, 8, 18, 200, window, hop)
+
+
+def _topk_phase_forms(n, k, minp, maxp, window, hop):
     torch = pytest.importorskip("torch")
     nwin = 300
-    s = synth.random_walk(nwin * n, seed=n + k + 17)
+    s = synth.random_walk((nwin - 1) * hop + n, seed=n + k + 17 + hop)
     dev = torch.device("cuda", 0)
     d_s = torch.from_numpy(s).to(dev)
     outs = []
     for v in (0, 1):
-        plan = bridge.Plan(0, n, n, nwin, "none", window, output="topk_phase")
+        plan = bridge.Plan(0, n, hop, nwin, "none", window, output="topk_phase")
         plan.set_topk(k, minp, maxp)
         plan.set_variant(v)
         d_o = torch.full((nwin * 6 * k,), float("nan"), dtype=torch.float64, device=dev)
@@ -478,12 +491,12 @@ def test_topk_phase_split_form(gpu_session, n, k, minp, maxp, window):
     a, b = outs
     same = a[:, :, 0] == b[:, :, 0]
     assert int((~same).sum()) <= 2
-    full_max = ref(s, n, n, "none", window).max(axis=1)[:, None]  # normalised like every parity bar
+    full_max = ref(s, n, hop, "none", window).max(axis=1)[:, None]  # normalised like every parity bar
     assert np.all(np.abs(np.where(same, a[:, :, 1] - b[:, :, 1], 0.0)) <= 1e-13 * full_max)
     got = outs[0]
-    want = oracle.batch_topk_phase(s, n, n, "none", window, 0, None, k, minp, maxp)
-    _topk_match(got[:, :, :4], want[:, :, :4], 1e-10, ref(s, n, n, "none", window).max(axis=1))
-    full = oracle.batch_phase(s, n, n, "none", window)
+    want = oracle.batch_topk_phase(s, n, hop, "none", window, 0, None, k, minp, maxp)
+    _topk_match(got[:, :, :4], want[:, :, :4], 1e-10, ref(s, n, hop, "none", window).max(axis=1))
+    full = oracle.batch_phase(s, n, hop, "none", window)
     for g in outs:
         for w in range(nwin):
             mag = np.sqrt(full[w, 0])
