@@ -76,7 +76,9 @@ def query(label, addr, base):
 
 
 def known(rec):
-    return rec["hip"] == "no error" or rec["hsa_type"] != "unknown"
+    """page-locked in HIP's view (hipPointerGetAttributes answers hipSuccess for pageable memory too, with type 0 =
+    hipMemoryTypeUnregistered) or known to ROCr"""
+    return (rec["hip"] == "no error" and rec["hip_type"] not in (None, 0)) or rec["hsa_type"] != "unknown"
 
 
 def scan(step, base, ranges, extra=()):
