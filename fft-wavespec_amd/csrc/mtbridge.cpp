@@ -1265,6 +1265,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return g.cfg[a].log2n > g.cfg[b].log2n; });
     SlideMix m{};
     m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
+    m.seed_lds = g.mode == 5;        // ablation: the round-4 seed FFTs
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1285,7 +1286,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     // floor, where halving only adds seeds) ran 5 % slower with them.  Mode 3: at every size; mode 4: never (A/B).
     const int last_l2 = g.cfg[order[n - 1]].log2n;
     const bool tail_half = policy && g.cfg[order[0]].log2n != last_l2 &&
-                           (g.mode == 3 || ((g.mode == 0 || g.mode == 2) && above_floor));
+                           (g.mode == 3 || ((g.mode == 0 || g.mode == 2 || g.mode == 5) && above_floor));
     Tables t4096;
     int st = get_tables(g.dev, 12, false, &t4096);
     if (st != MTB_OK) return st;
@@ -2236,8 +2237,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 4) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..4", (long long)group, mode);
+    if (!g || mode < 0 || mode > 5) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..5", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

@@ -74,6 +74,68 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
     }
 }
 
+// The same transform with the data in registers between passes (round 5): R = N / NT points per thread (8 at
+// N = 4096 / 2048, 4 at 1024 / 512 with two bins per thread), Stockham passes of radix R (the last one of the
+// remaining factor), the thread's pass-0 inputs x[t + NT r] straight from the caller's registers (no input
+// staging round trip), LDS only to exchange between passes.  N = 4096: 4 passes and 7 barriers instead of 6
+// radix-4 LDS passes, 12 barriers and the input staging -- the seeds were 14 % of every C5 task (33 of 242 us,
+// the r05c timeline) and all of the first round's latency.  Twiddles W_{Ns R}^k from the W_4096 quarter table
+// (k N / (Ns R) < N / 4), their powers by products (<= 7 steps).
+template <int LOG2N, int NT, int RP, int NS>
+__device__ __forceinline__ void reg_pass_write(d2 (&v)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT, Q = R / RP, TS = 4096 / N;
+    static_assert(Q * RP == R && RP >= 2, "pass geometry");
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = t + NT * q, k = j & (NS - 1);
+        d2 *a = v + q * RP;
+        if constexpr (NS > 1) {
+            const d2 w = twq[k * (N / (NS * RP)) * TS];
+            d2 wr = w;
+#pragma unroll
+            for (int r = 1; r < RP; ++r) {
+                a[r] = cmul(a[r], wr);
+                if (r + 1 < RP) wr = cmul(wr, w);
+            }
+        }
+        core::cpx<double> c[RP];  // by value: a d2 / cpx type pun through pointers breaks type-based alias analysis
+#pragma unroll
+        for (int r = 0; r < RP; ++r) c[r] = {a[r].x, a[r].y};
+        core::dft<double, RP>(c);
+#pragma unroll
+        for (int r = 0; r < RP; ++r) a[r] = d2{c[r].re, c[r].im};
+        const int o = (j - k) * RP + k;
+#pragma unroll
+        for (int r = 0; r < RP; ++r) buf[o + NS * r] = a[r];
+    }
+}
+template <int LOG2N, int NT, int NS>
+__device__ __forceinline__ void reg_passes(d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT;
+    if constexpr (NS < N) {
+        constexpr int RP = N / NS >= R ? R : N / NS;
+        d2 v[R];
+#pragma unroll
+        for (int q = 0; q < R / RP; ++q)
+#pragma unroll
+            for (int r = 0; r < RP; ++r) v[q * RP + r] = buf[t + NT * q + (N / RP) * r];
+        __syncthreads();
+        reg_pass_write<LOG2N, NT, RP, NS>(v, buf, twq, t);
+        __syncthreads();
+        reg_passes<LOG2N, NT, NS * RP>(buf, twq, t);
+    }
+}
+// a[r] = this thread's input x[t + NT r]; buf must be free (no reads pending).  Natural order in buf, ends after a
+// barrier.
+template <int LOG2N, int NT>
+__device__ __forceinline__ void fft_reg_sub(d2 (&a)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT;
+    static_assert(R == 4 || R == 8, "4 or 8 points per thread");
+    reg_pass_write<LOG2N, NT, R, 1>(a, buf, twq, t);
+    __syncthreads();
+    reg_passes<LOG2N, NT, R>(buf, twq, t);
+}
+
 // The kernel argument is read in place through the kernarg segment pointer (address space 4: scalar loads, any
 // index).  Passing the struct by reference to the device functions made the compiler copy its 1.4 KiB to scratch.
 typedef const __attribute__((address_space(4))) SlideMix *MixP;
@@ -99,7 +161,7 @@ __device__ __forceinline__ bool mix_seg(MixP m, int c, int64_t s, const void *&s
     return true;
 }
 
-template <typename T, int LOG2N, int NF, int DETREND, int BS>
+template <typename T, int LOG2N, int NF, int DETREND, int BS, int SR>
 __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, const d2 *twq, long long *trace) {
     // BS: bins per thread for N <= 1024 (2 by default, the per-length launches' geometry: 0.737 against 0.777 ms
     // for C5 at 4, which holds 4 / 8 segments side by side; profiles/r04/ab).  One-wave 512-point sub-workgroups
@@ -146,12 +208,23 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     double sum = 0.0;
 #pragma unroll
     for (int mm = 0; mm <= NM; ++mm) {
-        for (int i = t; i < N; i += NT) {
-            const double xi = on ? (double)x[i] - lvl : 0.0;
-            buf[i] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
+        if constexpr (SR) {  // register passes (default): the inputs straight from global memory into registers
+            d2 a[N / NT];
+#pragma unroll
+            for (int r = 0; r < N / NT; ++r) {
+                const int i = t + NT * r;
+                const double xi = on ? (double)x[i] - lvl : 0.0;
+                a[r] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
+            }
+            fft_reg_sub<LOG2N, NT>(a, buf, twq, t);
+        } else {  // mode 5 (ablation): the round-4 form, inputs staged in LDS and radix-4 passes through LDS
+            for (int i = t; i < N; i += NT) {
+                const double xi = on ? (double)x[i] - lvl : 0.0;
+                buf[i] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
+            }
+            __syncthreads();
+            fft_lds_sub<LOG2N, NT>(buf, twq, t);
         }
-        __syncthreads();
-        fft_lds_sub<LOG2N, NT>(buf, twq, t);
         const double s = mm == 0 ? m->s0 : (mm == 1 ? m->s1 : m->s2);
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -214,7 +287,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     __syncthreads();  // the staged uniforms' reads before the next task's writes
 }
 
-template <typename T, int NF, int DETREND, int BS>
+template <typename T, int NF, int DETREND, int BS, int SR>
 __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
     const MixP m = (MixP)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ d2 lds[4096];
@@ -246,10 +319,10 @@ __global__ __launch_bounds__(kMixNT, 4) void slide_mixed_kernel(SlideMix) {
             tr[1] = wall_clock64();
         }
         switch (l2) {
-        case 12: mix_task<T, 12, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
-        case 11: mix_task<T, 11, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
-        case 10: mix_task<T, 10, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
-        default: mix_task<T, 9, NF, DETREND, BS>(m, c, local, lds, twq, tr); break;
+        case 12: mix_task<T, 12, NF, DETREND, BS, SR>(m, c, local, lds, twq, tr); break;
+        case 11: mix_task<T, 11, NF, DETREND, BS, SR>(m, c, local, lds, twq, tr); break;
+        case 10: mix_task<T, 10, NF, DETREND, BS, SR>(m, c, local, lds, twq, tr); break;
+        default: mix_task<T, 9, NF, DETREND, BS, SR>(m, c, local, lds, twq, tr); break;
         }
         if (tr && tid == 0) tr[3] = wall_clock64();
     }
@@ -266,7 +339,7 @@ template <typename T, int NF, int DETREND, int BS> int resident_t(int dev) {
     static std::atomic<int> per_cu{0};
     int pc = per_cu.load(std::memory_order_relaxed);
     if (pc == 0) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND, BS>, kMixNT, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, slide_mixed_kernel<T, NF, DETREND, BS, 1>, kMixNT, 0) !=
                 hipSuccess ||
             pc <= 0)
             pc = 1;
@@ -283,9 +356,9 @@ template <typename T, int BS> int resident_nf(int nf, int detrend, int dev) {
     return mean ? resident_t<T, 3, kDetrendMean, BS>(dev) : resident_t<T, 3, kDetrendNone, BS>(dev);
 }
 
-template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
+template <typename T, int BS, int SR> hipError_t launch_nf(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
     const bool mean = detrend == kDetrendMean;
-#define MIX(NF_, D_) hipLaunchKernelGGL((slide_mixed_kernel<T, NF_, D_, BS>), dim3((unsigned)grid), dim3(kMixNT), 0, s, m)
+#define MIX(NF_, D_) hipLaunchKernelGGL((slide_mixed_kernel<T, NF_, D_, BS, SR>), dim3((unsigned)grid), dim3(kMixNT), 0, s, m)
     if (nf == 1) {
         if (mean) MIX(1, kDetrendMean);
         else MIX(1, kDetrendNone);
@@ -295,6 +368,9 @@ template <typename T, int BS> hipError_t launch_nf(const SlideMix &m, int nf, in
     }
 #undef MIX
     return hipGetLastError();
+}
+template <typename T, int BS> hipError_t launch_sr(const SlideMix &m, int nf, int detrend, int grid, hipStream_t s) {
+    return m.seed_lds ? launch_nf<T, BS, 0>(m, nf, detrend, grid, s) : launch_nf<T, BS, 1>(m, nf, detrend, grid, s);
 }
 
 }  // namespace
@@ -310,8 +386,8 @@ hipError_t launch_slide_mix(const SlideMix &m, int nf, int detrend, bool f32, in
         return hipErrorInvalidValue;
     for (int c = 0; c < m.nclass; ++c)
         if (m.log2n[c] < 9 || m.log2n[c] > 12 || m.seg[c] < 1 || !m.omega[c]) return hipErrorInvalidValue;
-    if (m.bsmall == 2) return f32 ? launch_nf<float, 2>(m, nf, detrend, grid, s) : launch_nf<double, 2>(m, nf, detrend, grid, s);
-    return f32 ? launch_nf<float, 4>(m, nf, detrend, grid, s) : launch_nf<double, 4>(m, nf, detrend, grid, s);
+    if (m.bsmall == 2) return f32 ? launch_sr<float, 2>(m, nf, detrend, grid, s) : launch_sr<double, 2>(m, nf, detrend, grid, s);
+    return f32 ? launch_sr<float, 4>(m, nf, detrend, grid, s) : launch_sr<double, 4>(m, nf, detrend, grid, s);
 }
 
 }  // namespace wsp

@@ -669,6 +669,38 @@ __device__ __forceinline__ void topk_rounds(int t, int kmin, int span, int k, XF
     }
 }
 
+// atan2 with its polynomial coefficients in SGPRs (the split phase record, round 5): the operations of OCML's
+// __ocml_atan2_f64 / __ocmlpriv_atanred_f64 (ROCm device library; min / max, one IEEE division, a degree-19 Horner
+// polynomial in t^2 by fma, the same selects for the quadrants, +-0 and the non-finite cases), so the results are
+// bit-identical to atan2() on the device; but the 20 coefficients are read from a constant table through a
+// per-window pinned pointer -- scalar loads into SGPRs, one SGPR operand per v_fma_f64 -- instead of being
+// materialised in 40 VGPRs and hoisted out of the window loop, which is what makes the inline atan2 spill (or, as
+// a call, forces the caller-saved registers around 18 calls to scratch) at the 168-VGPR bound of 3 waves per SIMD.
+__constant__ unsigned long long kAtanRed[20] = {
+    0x3EEBA404B5E68A13ull, 0xBF23E260BD3237F4ull, 0x3F4B2BB069EFB384ull, 0xBF67952DAF56DE9Bull, 0x3F7D6D43A595C56Full,
+    0xBF8C6EA4A57D9582ull, 0x3F967E295F08B19Full, 0xBF9E9AE6FC27006Aull, 0x3FA2C15B5711927Aull, 0xBFA59976E82D3FF0ull,
+    0x3FA82D5D6EF28734ull, 0xBFAAE5CE6A214619ull, 0x3FAE1BB48427B883ull, 0xBFB110E48B207F05ull, 0x3FB3B13657B87036ull,
+    0xBFB745D119378E4Full, 0x3FBC71C717E1913Cull, 0xBFC2492492376B7Dull, 0x3FC99999999952CCull, 0xBFD5555555555523ull};
+__device__ __forceinline__ double atan2_sc(double y, double x, const unsigned long long *cf) {
+    auto C = [&](int i) { return __builtin_bit_cast(double, cf[i]); };
+    constexpr double kPiO2 = 1.5707963267948966, kPi = 3.1415926535897931, k3PiO4 = 2.3561944901923448,
+                     kPiO4 = 0.78539816339744828;
+    const double ay = fabs(y), ax = fabs(x);
+    const double v = fmin(ax, ay) / fmax(ax, ay);
+    const double v2 = v * v;
+    double p = fma(v2, C(0), C(1));
+#pragma unroll
+    for (int i = 2; i < 20; ++i) p = fma(v2, p, C(i));
+    const double r = fma(v, v2 * p, v);
+    const bool xneg = __builtin_signbit(x);
+    double a = ax < ay ? kPiO2 - r : r;
+    a = xneg ? kPi - a : a;
+    a = y == 0.0 ? (xneg ? kPi : 0.0) : a;
+    if (ax == __builtin_inf() && ay == __builtin_inf()) a = xneg ? k3PiO4 : kPiO4;
+    if (__builtin_isnan(x) || __builtin_isnan(y)) a = __builtin_nan("");
+    return __builtin_copysign(a, y);
+}
+
 // atan2 as a call (the top-k + phase forms): inlined into the window loop, its ~19 fp64 polynomial coefficients are
 // materialised in VGPRs once and hoisted out of the loop (38 VGPRs held across the FFT: 20-212 B/lane of spills in
 // those forms); as a call they are rebuilt inside it, per call.  The full phase record (kOutPhase: 18 atan2 per
@@ -957,11 +989,11 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     for (; g < g_end; g += g_step) {
         // split top-k + phase: every address and twiddle that depends on t is recomputed per window instead of being
         // hoisted out of the window loop -- the 168-VGPR budget of 3 waves per SIMD has no room for them
-        if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(t));
+        if constexpr ((OUT == kOutTopKPhase || OUT == kOutPhase) && kSplit) asm volatile("" : "+v"(t));
         const int64_t w = g * WPB + slot;
         const bool active = w < a.n_windows;
         double xa[16], xb[16];
-        if constexpr (OUT == kOutTopKPhase && kSplit) {
+        if constexpr ((OUT == kOutTopKPhase || OUT == kOutPhase) && kSplit) {
             v2 rw[16];  // this window's samples only: nothing carried across windows
             load_group_buf<T, LOG2N>(a, w, t, rw);
 #pragma unroll
@@ -1221,7 +1253,9 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         // barrier), so that neither the twiddle load nor the 16 staging addresses and bound tests are issued at the
         // top of the window and held (spilled) across its FFT
         int tb0 = t;
-        if constexpr (OUT == kOutTopKPhase && kSplit) asm volatile("" : "+v"(tb0));
+        if constexpr ((OUT == kOutTopKPhase || OUT == kOutPhase) && kSplit) asm volatile("" : "+v"(tb0));
+        constexpr bool kPhaseSplit = OUT == kOutPhase && kSplit != 0;
+        double pim[kPhaseSplit ? 16 : 1];  // split phase record: Im X of the R2C slots, held until the slot is free
         const cpx<T> wt = a.tw[tb0];
         const cpx<T> wlo = tb0 == 0 ? cpx<T>{T(0.98078528040323044913), T(-0.19509032201612826785)} : wt;  // W_N^(B/2)
         const cpx<T> whi = tb0 == 0 ? cpx<T>{T(0), T(1)} : wt;  // W16^-4: slot s >= 4 of thread 0 -> W16^(s-4)
@@ -1266,6 +1300,12 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
                 if ((unsigned)ka <= (unsigned)(a.kmax + 1)) xrow[ka] = {kS1 * xa.re, kS1 * xa.im};
                 if ((unsigned)kb <= (unsigned)(a.kmax + 1)) xrow[kb] = {kS1 * xb.re, kS1 * xb.im};
+            } else if constexpr (kPhaseSplit) {  // split phase record: Re X to the split slot, Im in registers
+                double *srow = reinterpret_cast<double *>(lbase);
+                srow[pad16(ka)] = kS1 * xa.re;
+                srow[pad16(kb)] = kS1 * xb.re;
+                pim[s] = kS1 * xa.im;
+                pim[8 + s] = kS1 * xb.im;
             } else if constexpr (kPhase) {  // stage X for the phase / scan (AoS slot)
                 cpx<T> *xrow = reinterpret_cast<cpx<T> *>(lbase);
                 xrow[pad16(ka)] = {kS1 * xa.re, kS1 * xa.im};
@@ -1282,8 +1322,114 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         }
         // unwrapped phase / group delay of bins [16t, 16t + 16) (kept in registers
         // through the top-k scan for kOutTopKPhase)
+        if constexpr (kPhaseSplit) {
+            // Split phase record (round 5): the AoS form stages X as 16-B complex (35 KiB per window: two workgroups
+            // per CU) and holds [P | phase | delay] for 16 bins at once (241 VGPRs: two waves per SIMD).  Here the
+            // window's 17 KiB split slot takes Re X, each thread reads its 18 consecutive bins (16 + two neighbours),
+            // then Im X the same way; the rows are computed and written one after another (P, then the unwrapped
+            // phase, then the group delay), so at most one row of 16 values is live: 3 waves per SIMD.  Same
+            // arithmetic as phase_chunk (the unwrap decisions from the atan2 values, K an exact integer prefix count,
+            // u = phi + 2 pi K by one fma, CalculateGroupDelay's central difference clamped to +-100).
+            constexpr double kPi = 3.14159265358979323846, k2Pi = 2.0 * kPi;
+            double *srow = reinterpret_cast<double *>(lbase);
+            const int k0 = 16 * t;
+            double re[18], ph[18];
+            __syncthreads();  // Re row complete
+#pragma unroll
+            for (int j = 0; j < 18; ++j) {
+                const int k = k0 - 1 + j;
+                re[j] = (k >= 0 && k < M) ? srow[pad16(k)] : 0.0;  // bin M: the zeroed upper half
+            }
+            __syncthreads();  // Re reads done: the slot takes Im
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                int ka = tb0 + B * s, kb = M - ka;
+                if (tb0 == 0) {
+                    ka = s < 4 ? B / 2 + B * s : B * (s - 4);
+                    kb = s == 4 ? M / 2 : M - ka;
+                }
+                srow[pad16(ka)] = pim[s];
+                srow[pad16(kb)] = pim[8 + s];
+            }
+            __syncthreads();
+            double im[18], pwr[16];
+#pragma unroll
+            for (int j = 0; j < 18; ++j) {
+                const int k = k0 - 1 + j;
+                im[j] = (k >= 0 && k < M) ? srow[pad16(k)] : 0.0;
+                if (j >= 1 && j <= 16) pwr[j - 1] = re[j] * re[j] + im[j] * im[j];
+            }
+            // [P | unwrapped phase | group delay] rows through the slot: pairs 16-B aligned (two pad doubles per 32
+            // inside the SLOT doubles), written with contiguous 16-B NT stores (1 KiB per wave instruction)
+            auto pidx2 = [](int k) { return k + 2 * (k >> 5); };
+            auto put = [&](const double(&val)[16], int row) {
+                __syncthreads();  // previous reads of the slot are done
+#pragma unroll
+                for (int j = 0; j < 16; j += 2)
+                    *reinterpret_cast<v2 *>(srow + pidx2(16 * t + j)) = v2{val[j], val[j + 1]};
+                __syncthreads();
+                if (active) {
+                    T *dst = a.out + w * (int64_t)(3 * M) + row * M;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = 2 * (t + TPW * j);
+                        __builtin_nontemporal_store(*reinterpret_cast<const v2 *>(srow + pidx2(k)),
+                                                    reinterpret_cast<v2 *>(dst + k));
+                    }
+                }
+            };
+            put(pwr, 0);  // the power row first: nothing but (re, im) is held across the 18 atan2
+            const unsigned long long *cf = kAtanRed;
+            asm volatile("" : "+s"(cf));  // per window: the coefficients' scalar loads stay inside the window loop
+#pragma unroll
+            for (int j = 0; j < 18; ++j) ph[j] = atan2_sc(im[j], re[j], cf);
+            int cj[17];  // correction of bins k0 .. k0 + 16 (UnwrapPhase :1068-1077)
+#pragma unroll
+            for (int j = 0; j < 17; ++j) {
+                const double diff = ph[j + 1] - ph[j];
+                cj[j] = (k0 + j == 0) ? 0 : diff > kPi ? -1 : diff < -kPi ? 1 : 0;
+            }
+            int sum = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) sum += cj[j];
+            constexpr int SW = TPW < 64 ? TPW : 64;
+            const int lt = t & (SW - 1);
+            int incl = sum;
+#pragma unroll
+            for (int d = 1; d < SW; d <<= 1) {
+                const int up = __shfl_up(incl, d, SW);
+                if (lt >= d) incl += up;
+            }
+            int K = incl - sum;  // corrections of every bin < k0
+            if constexpr (TPW >= 128) {  // + the totals of the window's earlier waves
+                int *sb = reinterpret_cast<int *>(scanbuf + 8);
+                __syncthreads();  // the previous window's reads of sb are done
+                if (lt == 63) sb[t >> 6] = incl;
+                __syncthreads();
+                for (int i = 0; i < (t >> 6); ++i) K += sb[i];
+            }
+            const double um1 = fma((double)K, k2Pi, ph[0]);  // u[k0 - 1]
+            double uu[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                K += cj[j];
+                uu[j] = fma((double)K, k2Pi, ph[j + 1]);
+            }
+            const double upc = fma((double)(K + cj[16]), k2Pi, ph[17]);  // u[k0 + 16]
+            put(uu, 1);
+            double gdd[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {  // :1102-1119
+                const double lo = j ? uu[j - 1] : um1, hi = j < 15 ? uu[j + 1] : upc;
+                double g = (k0 + j == 0) ? -(uu[1] - uu[0]) : -(hi - lo) / 2.0;
+                if (g > 100.0) g = 100.0;
+                if (g < -100.0) g = -100.0;
+                gdd[j] = g;
+            }
+            put(gdd, 2);
+        }
         double pw[OUT == kOutPhase ? 16 : 1], u[OUT == kOutPhase ? 16 : 1], gd[OUT == kOutPhase ? 16 : 1];
-        if constexpr (OUT == kOutPhase) {
+        if constexpr (OUT == kOutPhase && !kPhaseSplit) {
             const cpx<double> *xrow = reinterpret_cast<const cpx<double> *>(lbase);
             __syncthreads();  // X row complete
             phase_chunk<LOG2N>(xrow, t, scanbuf, pw, u, gd);

@@ -100,7 +100,8 @@ print('$cfg', '$extra', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step']
         cat $O/kalman_bench.log
         ;;
     harness)
-        hl=$O/harness_${val//,/_}.log
+        hn=${val//,/_}
+        hl=$O/harness_${hn//\//_}.log
         run 300 $hl $hl python3 scripts/${val//,/ }
         cat $hl
         ;;
