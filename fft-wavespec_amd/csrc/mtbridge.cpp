@@ -584,6 +584,8 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             A.topk = c.topk;
             A.ws = d_ws;
             A.flags = c.scan_flags;
+            // seed chains of <= 256 windows (variant 6: one FFT seed per segment, the round-4 form)
+            A.seed_chain = c.variant == 6 ? 1 : (int)std::min<int64_t>(16, 1 + 256 / A.seg);
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }

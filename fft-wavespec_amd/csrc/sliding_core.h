@@ -342,20 +342,35 @@ __global__ __launch_bounds__(seed_nt<LOG2N>()) void slide_seed_kernel(SlideArgs 
 // Stockham passes with LDS only between passes -- 2 exchanges at N = 2048 / 4096 against 6 / 7 LDS round trips
 // of fft_lds at N/4 threads), one transform m at a time, every output in natural order to LDS and the band read
 // back: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}) as slide_seed_kernel (N >= 1024).
-template <int LOG2N, int NF, int DETREND>
+//
+// Seed chains (round 5): a workgroup seeds G = a.seed_chain consecutive segments -- the first by the FFTs, each next one
+// by sliding the band's trackers a.seg windows on from the previous (slide_step, the uniforms of stage_uniforms: the
+// same operations the scan kernel applies, so a chained seed is exactly what the scan wave of the previous segment
+// holds after sliding across the seam, as if the segments were one).  The segment count of the scan (one wave per
+// segment, a full round of resident waves) no longer sets the number of FFT seeds: a one-eighth C4 shard has 2048
+// segments of 64 windows and seeded every one by two 2048-point FFTs, a fixed ~44 us beside a ~45 us scan
+// (profiles/r04/shards.json: C4 top-8 3.7x at 8 ranks).  Chains are at most 256 windows long (as the rounding of a
+// 256-window segment); the workgroup's threads keep their bins' trackers (j = t + TP i < span) in registers.
+template <int LOG2N, int NF, int DETREND, int JB>
 __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideArgs a) {
     using G = wg::LGeo<LOG2N>;
     constexpr int N = 1 << LOG2N, M = N / 2, TP = G::TP, NM = (NF - 1) / 2, R = wg::last_radix<LOG2N>();
+    constexpr int REC = Rec<NF>::n;  // JB: band bins per thread, span <= JB TP (launch_topk_t)
     __shared__ core::cpx<double> lds[G::SLOT];
     const int t = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * a.seg;
+    const int chain = a.seed_chain > 1 ? a.seed_chain : 1;
+    const int64_t sg0 = (int64_t)blockIdx.x * chain;  // this workgroup's first segment
+    const int64_t w0 = sg0 * a.seg;
     if (w0 >= a.n_windows) return;
     const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
     const core::cpx<double> *__restrict__ tw = static_cast<const core::cpx<double> *>(a.twiddle);
     const d2 *__restrict__ mod = static_cast<const d2 *>(a.omega) + (NF + 1) * M;  // [NM][N] e^{-j m th i}
     const double lvl = DETREND == kDetrendMean ? x[0] : 0.0;
-    d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + blockIdx.x * slide_topk_seed_stride(NF, a.span);
+    const int64_t stride = slide_topk_seed_stride(NF, a.span);
+    d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + sg0 * stride;
     const int span = a.span, kmin = a.kmin;
+    d2 trk[JB][NF];  // the chain's trackers of bins kmin + t + TP i
+    double sum = 0.0;
     double xs[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) xs[r] = x[t + TP * r] - lvl;
@@ -379,19 +394,70 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             for (int r = 0; r < R; ++r) lds[core::pad16(t + TP * q + (N / R) * r)] = v[q * R + r];
         __syncthreads();
         const double s = m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2);
-        for (int j = t; j < span; j += TP) {
+#pragma unroll
+        for (int i = 0; i < JB; ++i) {
+            const int j = t + TP * i;
+            if (j >= span) continue;
             const int k = kmin + j;
             const core::cpx<double> yp = lds[core::pad16(k)];
             if (m == 0) {
-                ws[j] = s * d2{yp.re, yp.im};
+                trk[i][0] = s * d2{yp.re, yp.im};
+                ws[j] = trk[i][0];
             } else {
                 const core::cpx<double> ym = lds[core::pad16((N - k) & (N - 1))];
-                ws[(2 * m - 1) * span + j] = s * d2{yp.re, yp.im};
-                ws[(2 * m) * span + j] = s * d2{ym.re, -ym.im};
+                trk[i][2 * m - 1] = s * d2{yp.re, yp.im};
+                trk[i][2 * m] = s * d2{ym.re, -ym.im};
+                ws[(2 * m - 1) * span + j] = trk[i][2 * m - 1];
+                ws[(2 * m) * span + j] = trk[i][2 * m];
             }
         }
-        if (m == 0 && t == 0) ws[NF * span] = d2{lds[0].re, lvl};  // sum of x - L (mean path), L
+        if (m == 0) {
+            sum = lds[0].re;  // sum of x - L (mean path)
+            if (t == 0) ws[NF * span] = d2{sum, lvl};  // and L
+        }
         __syncthreads();  // the band reads before the next transform's exchanges
+    }
+    if (chain == 1) return;
+    d2 om[JB][NF];
+    const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
+#pragma unroll
+    for (int i = 0; i < JB; ++i) {
+        const int j = t + TP * i;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            om[i][f] = j < span ? omega[f * M + kmin + j] : d2{1.0, 0.0};
+            if (j >= span) trk[i][f] = d2{0.0, 0.0};
+        }
+    }
+    const int64_t seg = a.seg;
+    for (int g = 1; g < chain; ++g) {
+        const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
+        if (w0 + wsg0 >= a.n_windows) break;
+#pragma unroll 1
+        for (int64_t st = wsg0 - seg; st < wsg0; ++st) {  // window st -> st + 1 (stage_uniforms' arithmetic)
+            const double xw = x[st] - lvl, xn = x[st + N] - lvl;
+            double r[REC];
+            r[0] = a.s0 * (xn - xw);
+            if constexpr (NF >= 3) {
+                r[1] = a.s1 * (xn * a.c1 - xw);
+                r[2] = -(a.s1 * (xn * a.sn1));
+            }
+            if constexpr (NF >= 5) {
+                r[3] = a.s2 * (xn * a.c2 - xw);
+                r[4] = -(a.s2 * (xn * a.sn2));
+            }
+            r[REC - 1] = xn - xw;
+            slide_step<JB, NF, DETREND>(trk, om, r, sum);
+        }
+        d2 *__restrict__ wsg = ws + g * stride;
+#pragma unroll
+        for (int i = 0; i < JB; ++i) {
+            const int j = t + TP * i;
+            if (j >= span) continue;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) wsg[f * span + j] = trk[i][f];
+        }
+        if (t == 0) wsg[NF * span] = d2{sum, lvl};  // the chain's level L (the scan's uniforms follow x - L)
     }
 }
 
@@ -842,7 +908,13 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {
     const int64_t grid = (a.n_windows + a.seg - 1) / a.seg;
     if constexpr (LOG2N >= 10) {
-        hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3((1 << LOG2N) / 16), 0, s, a);
+        const int chain = a.seed_chain > 1 ? a.seed_chain : 1;
+        constexpr int TP = (1 << LOG2N) / 16;
+        const dim3 sg((unsigned)((grid + chain - 1) / chain)), sb(TP);
+        if (a.span <= TP) hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND, 1>), sg, sb, 0, s, a);
+        else if (a.span <= 2 * TP) hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND, 2>), sg, sb, 0, s, a);
+        else if (a.span <= 4 * TP) hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND, 4>), sg, sb, 0, s, a);
+        else hipLaunchKernelGGL((slide_seed_r_kernel<LOG2N, NF, DETREND, (kSlideTopkMaxSpan + TP - 1) / TP>), sg, sb, 0, s, a);
     } else {
         hipLaunchKernelGGL((slide_seed_kernel<double, LOG2N, NF, DETREND>), dim3((unsigned)grid), dim3(seed_nt<LOG2N>()), 0,
                            s, a);

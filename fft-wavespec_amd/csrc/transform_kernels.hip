@@ -123,7 +123,12 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, 2) void inverse_kernel(const dou
 // by two threads, the second time from L2), instead of staging all of conj Z through LDS and reading it back
 // -- one LDS round trip and one barrier fewer -- and, with SPLIT, the real/imaginary split exchanges of the
 // forward kernel (half the LDS, 3 waves per SIMD).  Z_(M/2) = conj X_(M/2) and the DC term as above.
-template <int LOG2N, int SPLIT>
+// PAIRED (round 5, the default): the 16 elements are loaded in the order r = 0, 15, 1, 14, ... -- element k's mirror
+// M - k is element 15 - r of the partner thread TPW - t (the other wave of the window), so the two reads of every
+// X_k (once as k, once as the partner's mirror) fall one load step apart instead of up to 15, and the second one
+// hits the line the first brought into L2 (in natural order 0.3 of the second reads went to HBM: PMC 2.79 GB of
+// reads per step against 2.15 GB algorithmic, profiles/r04/inverse_*); variant 3 keeps the natural order.
+template <int LOG2N, int SPLIT, bool PAIRED = true>
 __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_direct_kernel(
     const double *__restrict__ in, double *__restrict__ out, const cpx<double> *__restrict__ tw, int64_t n_windows,
     int64_t n_groups) {
@@ -149,7 +154,8 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_dire
 #pragma unroll
         for (int q = 0; q < BPT0; ++q)
 #pragma unroll
-            for (int r = 0; r < R0; ++r) {
+            for (int i = 0; i < R0; ++i) {
+                const int r = PAIRED ? ((i & 1) ? R0 - 1 - (i >> 1) : (i >> 1)) : i;
                 const int k = (t + TPW * q) + (M / R0) * r;
                 const v2 pa = *reinterpret_cast<const v2 *>(xin + 2 * k);
                 const v2 pb = *reinterpret_cast<const v2 *>(xin + 2 * ((M - k) & (M - 1)));
@@ -163,7 +169,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_dire
                 const cpx<T> z = {e.re - o.im, -(e.im + o.re)};  // conj Z_k
                 v[q * R0 + r] = k == M / 2 ? cpx<T>{pa.x, pa.y} : z;  // conj(conj X_(M/2))
                 // at most 4 elements' loads in flight: hoisting all 32 sample and 16 twiddle loads spills
-                if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
         for (int q = 0; q < BPT0; ++q) dft<T, R0>(&v[q * R0]);
@@ -264,7 +270,8 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
     if (L.n_windows <= 0) return hipSuccess;
     const auto *tw = static_cast<const cpx<double> *>(L.twiddle);
     // the C2R pre-step in registers with the split exchange at N = 2048 .. 8192 (inverse_direct_kernel); variant 1
-    // = the LDS pre-step kernel (round 1-3 form), variant 2 = the register pre-step with the AoS exchange
+    // = the LDS pre-step kernel (round 1-3 form), variant 2 = the register pre-step with the AoS exchange, variant 3 =
+    // the element loads in natural order (round 4; the default pairs each element's two reads in time)
 #define INV_CASE(LG)                                                                                          \
     case LG: {                                                                                                \
         const int64_t groups = (L.n_windows + Geo<LG>::WPB - 1) / Geo<LG>::WPB;                               \
@@ -276,6 +283,9 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
         else if (L.variant == 2)                                                                              \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 0>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
                                L.out, tw, L.n_windows, groups);                                               \
+        else if (L.variant == 3)                                                                              \
+            hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, false>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, \
+                               L.in, L.out, tw, L.n_windows, groups);                                         \
         else                                                                                                  \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 2>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
                                L.out, tw, L.n_windows, groups);                                               \

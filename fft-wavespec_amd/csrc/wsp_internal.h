@@ -135,6 +135,8 @@ struct SlideArgs {
     unsigned char *flags; // probe-threshold top-k scan: per-window path (wsp_plan_set_scan_flags), nullptr = off
     double share;         // launches running side by side (grouped plan on several streams): the launcher's
                           // segments fill 1/share of the resident workgroup slots; 0 / 1 = all of them
+    int seed_chain;       // top-k seeds (N >= 1024): segments per seed workgroup -- one FFT seed, the next ones by
+                          // sliding the band's trackers seg windows at a time (<= 1: one FFT seed per segment)
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
 // Grouped launch: several series of the same window length (the symbols of one length in a

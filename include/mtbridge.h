@@ -338,7 +338,11 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
- *    with the AoS exchange; 0 = the pre-step in registers, split exchange;
+ *    with the AoS exchange; 3 = 0 with the element loads in natural order
+ *    (round 4); 0 = the pre-step in registers, split exchange, each element's
+ *    two reads (as X_k and as a mirror X_(M-k)) one load step apart;
+ *  - MTB_OUT_PHASE records at N = 2048 / 4096 without IIR detrend: 1 = the
+ *    AoS form (two waves per SIMD) instead of the split-exchange form (round 5);
  *  - MTB_OUT_TOPK_PHASE records (FFT kernel): 1 = the AoS form (two waves per
  *    SIMD, every thread's phase chunk) instead of the split-exchange one-wave
  *    scan + one-wave winners' phases. */

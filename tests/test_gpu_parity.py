@@ -262,6 +262,44 @@ def _topk_match(got, want, tol, full_max):
         assert np.max(np.abs(got[w, same, 2:] - want[w, same, 2:]), initial=0.0) <= tol * amp * 10
 
 
+@pytest.mark.parametrize("n", [2048, 4096])
+@pytest.mark.parametrize("detrend,window,hop_of", [("none", "hann", "n"), ("none", "blackman", "1"),
+                                                   ("mean", "hamming", "37"), ("none", "none", "n+5"),
+                                                   ("mean", "bartlett", "n/4")])
+def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
+    """Round 5: the split-exchange phase record (default at N = 2048 / 4096 without IIR: Re and Im of X staged
+    through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with its
+    coefficients in SGPRs -- 3 waves per SIMD) against the AoS form (wsp_plan_set_variant 1) and the oracle, over
+    every window: power rows to 1e-13 of each other (the forms evaluate the cosine windows differently)
+    and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of test_phase_output."""
+    torch = pytest.importorskip("torch")
+    hop = {"1": 1, "37": 37, "n/4": n // 4, "n": n, "n+5": n + 5}[hop_of]
+    nwin = 90
+    s = synth.random_walk((nwin - 1) * hop + n, seed=n + hop)
+    dev = torch.device("cuda", 0)
+    d_s = torch.from_numpy(s).to(dev)
+    outs = []
+    for v in (0, 1):
+        plan = bridge.Plan(0, n, hop, nwin, detrend, window, output="phase")
+        plan.set_variant(v)
+        d_o = torch.full((nwin * 3 * (n // 2),), float("nan"), dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(d_o.view(nwin, 3, n // 2).cpu().numpy())
+        plan.close()
+    split, aos = outs
+    assert np.isfinite(split).all()
+    scale = aos[:, 0].max(axis=1, keepdims=True)
+    assert np.all(np.abs(split[:, 0] - aos[:, 0]) <= 1e-13 * scale)
+    want = oracle.batch_phase(s, n, hop, detrend, window)
+    for got in outs:
+        assert oracle.rel_err(got[:, 0], want[:, 0]) <= 1e-10
+        for w in range(nwin):
+            mag = np.sqrt(want[w, 0])
+            m = _unwrap_match(got[w, 1], want[w, 1], mag)
+            _delay_match(got[w, 2], want[w, 2], mag, m)
+
+
 @pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),
                                                (256, 256, 16, 2, 10000), (512, 512, 8, 300, 400),
                                                (16384, 16384, 8, 18, 52), (8192, 100, 64, 2, 8192)])
@@ -325,9 +363,10 @@ def test_inverse_round_trip_single(gpu_session, n):
 @pytest.mark.parametrize("n", [1024, 2048, 4096, 8192])
 def test_inverse_forms(gpu_session, n):
     """The inverse plan's kernel forms (wsp_plan_set_variant): 0 = the C2R pre-step in registers with the split
-    exchange (default at N = 2048 .. 8192), 1 = the pre-step through LDS (round-1 form), 2 = registers + the
-    AoS exchange: each against the oracle (1e-12 of the window's max) and within 1e-14 of each other, on a ragged
-    batch (the last workgroup's window slots past the end)."""
+    exchange (default at N = 2048 .. 8192; each element's two reads paired in time, round 5), 1 = the pre-step
+    through LDS (round-1 form), 2 = registers + the AoS exchange, 3 = the default with the loads in natural order
+    (round 4; bit-identical to 0: only the load order differs): each against the oracle (1e-12 of the window's max)
+    and within 1e-14 of each other, on a ragged batch (the last workgroup's window slots past the end)."""
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(n + 1)
     w = 333
@@ -335,7 +374,7 @@ def test_inverse_forms(gpu_session, n):
     dev = torch.device("cuda", 0)
     d_in = torch.from_numpy(spec).to(dev)
     outs = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         plan = bridge.Plan.inverse(0, n, w)
         plan.set_variant(v)
         d_o = torch.full((w * n,), float("nan"), dtype=torch.float64, device=dev)
@@ -350,6 +389,8 @@ def test_inverse_forms(gpu_session, n):
     scale = np.abs(outs[1]).max(axis=1, keepdims=True)
     assert np.all(np.abs(outs[0] - outs[1]) <= 1e-14 * scale)
     assert np.all(np.abs(outs[2] - outs[1]) <= 1e-14 * scale)
+    if n >= 2048:
+        assert np.array_equal(outs[3], outs[0])
 
 
 def test_inverse_plan_full_size(gpu_session):
@@ -410,7 +451,7 @@ def _delay_match(got, want, mag, m):
     assert np.all((np.abs(got - want) <= tn)[cond])
 
 
-@pytest.mark.parametrize("n", [32, 256, 1024, 4096, 16384])
+@pytest.mark.parametrize("n", [32, 256, 1024, 2048, 4096, 16384])
 @pytest.mark.parametrize("detrend,period", [("none", 0), ("mean", 0), ("iir", 1024)])
 def test_phase_output(gpu_session, n, detrend, period):
     """MTB_OUT_PHASE: [P | unwrapped phase | group delay] (1.0.4-new.mq5:1040-1120 at :3225-3227)."""
@@ -425,6 +466,44 @@ def test_phase_output(gpu_session, n, detrend, period):
         mag = np.sqrt(want[w, 0])
         m = _unwrap_match(got[w, 1], want[w, 1], mag)
         _delay_match(got[w, 2], want[w, 2], mag, m)
+
+
+@pytest.mark.parametrize("n", [2048, 4096])
+@pytest.mark.parametrize("detrend,window,hop_of", [("none", "hann", "n"), ("none", "blackman", "1"),
+                                                   ("mean", "hamming", "37"), ("none", "none", "n+5"),
+                                                   ("mean", "bartlett", "n/4")])
+def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
+    """Round 5: the split-exchange phase record (default at N = 2048 / 4096 without IIR: Re and Im of X staged
+    through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with its
+    coefficients in SGPRs -- 3 waves per SIMD) against the AoS form (wsp_plan_set_variant 1) and the oracle, over
+    every window: power rows to 1e-13 of each other (the forms evaluate the cosine windows differently)
+    and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of test_phase_output."""
+    torch = pytest.importorskip("torch")
+    hop = {"1": 1, "37": 37, "n/4": n // 4, "n": n, "n+5": n + 5}[hop_of]
+    nwin = 90
+    s = synth.random_walk((nwin - 1) * hop + n, seed=n + hop)
+    dev = torch.device("cuda", 0)
+    d_s = torch.from_numpy(s).to(dev)
+    outs = []
+    for v in (0, 1):
+        plan = bridge.Plan(0, n, hop, nwin, detrend, window, output="phase")
+        plan.set_variant(v)
+        d_o = torch.full((nwin * 3 * (n // 2),), float("nan"), dtype=torch.float64, device=dev)
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(d_o.view(nwin, 3, n // 2).cpu().numpy())
+        plan.close()
+    split, aos = outs
+    assert np.isfinite(split).all()
+    scale = aos[:, 0].max(axis=1, keepdims=True)
+    assert np.all(np.abs(split[:, 0] - aos[:, 0]) <= 1e-13 * scale)
+    want = oracle.batch_phase(s, n, hop, detrend, window)
+    for got in outs:
+        assert oracle.rel_err(got[:, 0], want[:, 0]) <= 1e-10
+        for w in range(nwin):
+            mag = np.sqrt(want[w, 0])
+            m = _unwrap_match(got[w, 1], want[w, 1], mag)
+            _delay_match(got[w, 2], want[w, 2], mag, m)
 
 
 @pytest.mark.parametrize("n,hop,k,minp,maxp", [(4096, 4096, 8, 18, 200), (1024, 1, 8, 9, 200), (64, 7, 3, 4, 64),

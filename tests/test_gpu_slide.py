@@ -267,6 +267,45 @@ def test_slide_topk_scan_forms_identical(gpu_session, n, pmin, pmax, seg):
     _topk_bars(outs[0], want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
 
 
+@pytest.mark.parametrize("n,detrend,window,seg,nwin", [(2048, "none", "hann", 0, 131072), (2048, "none", "hann", 32, 5000),
+                                                      (2048, "mean", "hamming", 7, 3001), (1024, "none", "blackman", 64, 4099),
+                                                      (4096, "mean", "hann", 100, 2999), (2048, "none", "none", 2048, 4100)])
+def test_slide_topk_seed_chains(gpu_session, n, detrend, window, seg, nwin):
+    """Round 5: the top-k seeds in chains (one FFT seed per chain of <= 256 windows, the next segments' seeds by
+    sliding the band's trackers on, wsp_plan_set_variant 6 = one FFT seed per segment): against the unchained form and
+    the oracle on every window -- the policy's segments of a one-eighth C4 shard (131072 windows: chains of 5 segments of
+    64), short segments (chains of 16 x 7 windows, the chain cap), a ragged last chain, the mean detrend (the chain's
+    level L carried in the seed record) and a segment too long to chain."""
+    torch = pytest.importorskip("torch")
+    s = synth.random_walk(nwin + n - 1, seed=n + seg + 5)
+    outs = []
+    for v in (0, 6):
+        plan = bridge.Plan(0, n, 1, nwin, detrend, window, output="topk")
+        plan.set_topk(8, 18.0, 200.0)
+        plan.set_algorithm("slide")
+        plan.set_variant(v)
+        if seg:
+            plan.set_slide_segment(seg)
+        outs.append(_run(plan, s, torch).reshape(nwin, 8, 4))
+        plan.close()
+    chained, single = outs
+    same = chained[:, :, 0] == single[:, :, 0]
+    assert (~same).sum() <= 8
+    if nwin > 20000:  # the full shard: the oracle on a spread of windows (every 64-window segment seam near 0 / mid / end)
+        idx = np.unique(np.r_[0:200, nwin // 2 - 100:nwin // 2 + 100, nwin - 200:nwin])
+        sub = np.concatenate([s[i:i + n] for i in idx])
+        want = oracle.batch_topk(sub, n, n, detrend, window, 0, None, 8, 18.0, 200.0)
+        spec = oracle.batch_spectrum(sub, n, n, detrend, window)
+        kmin, kmax = oracle.band(n)
+        _topk_bars(chained[idx], want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+        return
+    want = oracle.batch_topk(s, n, 1, detrend, window, 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, detrend, window)
+    kmin, kmax = oracle.band(n)
+    for got in outs:
+        _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
 @pytest.mark.parametrize("case", ["zeros", "ones_mean", "zeros_then_walk"])
 def test_slide_topk_exact_ties(gpu_session, case):
     """Exactly tied band powers: a zero series (every tracker stays exactly 0), a constant 1.0 with
