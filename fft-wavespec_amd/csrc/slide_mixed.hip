@@ -80,7 +80,8 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
 // staging round trip), LDS only to exchange between passes.  N = 4096: 4 passes and 7 barriers instead of 6
 // radix-4 LDS passes, 12 barriers and the input staging -- the seeds were 14 % of every C5 task (33 of 242 us,
 // the r05c timeline) and all of the first round's latency.  Twiddles W_{Ns R}^k from the W_4096 quarter table
-// (k N / (Ns R) < N / 4), their powers by products (<= 7 steps).
+// (k N / (Ns R) < N / 4 for R = 4 / 8; a final radix-2 pass folds its upper quarter by W^(N/4) = -i), their powers
+// by products (<= 7 steps).
 template <int LOG2N, int NT, int RP, int NS>
 __device__ __forceinline__ void reg_pass_write(d2 (&v)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
     constexpr int N = 1 << LOG2N, R = N / NT, Q = R / RP, TS = 4096 / N;
@@ -90,7 +91,16 @@ __device__ __forceinline__ void reg_pass_write(d2 (&v)[(1 << LOG2N) / NT], d2 *b
         const int j = t + NT * q, k = j & (NS - 1);
         d2 *a = v + q * RP;
         if constexpr (NS > 1) {
-            const d2 w = twq[k * (N / (NS * RP)) * TS];
+            // W_N^m, m = k N / (Ns R): below N/4 (the quarter table) for R = 4 / 8; a last radix-2 pass reaches
+            // m < N/2, whose upper quarter is W_N^(m - N/4) (-i)
+            const int m = k * (N / (NS * RP));
+            d2 w;
+            if constexpr (RP == 2) {
+                const d2 q = twq[(m & (N / 4 - 1)) * TS];
+                w = m < N / 4 ? q : d2{q.y, -q.x};
+            } else {
+                w = twq[m * TS];
+            }
             d2 wr = w;
 #pragma unroll
             for (int r = 1; r < RP; ++r) {

@@ -429,26 +429,21 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             if (j >= span) trk[i][f] = d2{0.0, 0.0};
         }
     }
+    // the chain's per-step uniforms, all at once into LDS (stage_uniforms: every thread a share of the steps), then
+    // the sequential slide reads them by broadcast -- loading x[w], x[w + N] inside the dependent loop put a global
+    // load latency on every step (C4 top-8 0.355 -> 0.440 ms in the first version, r05f)
     const int64_t seg = a.seg;
+    const int64_t last = a.n_windows - 1 - w0;  // no step past the batch's last window
+    const int nsteps = (int)((chain - 1) * seg < last ? (chain - 1) * seg : last);
+    double *u = reinterpret_cast<double *>(lds);
+    static_assert(256 * REC <= G::SLOT * 2, "a chain's uniforms fit the FFT's LDS");
+    stage_uniforms<double, NF, N>(a, x, lvl, 0, nsteps, nsteps + 1, u, t, TP);
+    __syncthreads();
     for (int g = 1; g < chain; ++g) {
         const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
-        if (w0 + wsg0 >= a.n_windows) break;
+        if (wsg0 > nsteps) break;
 #pragma unroll 1
-        for (int64_t st = wsg0 - seg; st < wsg0; ++st) {  // window st -> st + 1 (stage_uniforms' arithmetic)
-            const double xw = x[st] - lvl, xn = x[st + N] - lvl;
-            double r[REC];
-            r[0] = a.s0 * (xn - xw);
-            if constexpr (NF >= 3) {
-                r[1] = a.s1 * (xn * a.c1 - xw);
-                r[2] = -(a.s1 * (xn * a.sn1));
-            }
-            if constexpr (NF >= 5) {
-                r[3] = a.s2 * (xn * a.c2 - xw);
-                r[4] = -(a.s2 * (xn * a.sn2));
-            }
-            r[REC - 1] = xn - xw;
-            slide_step<JB, NF, DETREND>(trk, om, r, sum);
-        }
+        for (int64_t st = wsg0 - seg; st < wsg0; ++st) slide_step<JB, NF, DETREND>(trk, om, u + st * REC, sum);
         d2 *__restrict__ wsg = ws + g * stride;
 #pragma unroll
         for (int i = 0; i < JB; ++i) {
