@@ -584,8 +584,10 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             A.topk = c.topk;
             A.ws = d_ws;
             A.flags = c.scan_flags;
-            // seed chains of <= 256 windows (variant 6: one FFT seed per segment, the round-4 form)
-            A.seed_chain = c.variant == 6 ? 1 : (int)std::min<int64_t>(16, 1 + 256 / A.seg);
+            // variant 6 (ablation): seed chains of <= 256 windows -- one FFT seed per chain, the next segments' seeds
+            // by sliding the band on; slower than one FFT seed per segment (C4 top-8 0.404 against 0.355 ms, a 1/8
+            // shard 0.113 against 0.096, r05g: the chain's serial slide steps outlast the parallel FFT seeds)
+            A.seed_chain = c.variant == 6 ? (int)std::min<int64_t>(16, 1 + 256 / A.seg) : 1;
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }
@@ -620,7 +622,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
     L.topk = c.topk;
     L.kmin = c.kmin;
     L.kmax = c.kmax;
-    L.variant = c.output == MTB_OUT_TOPK_PHASE ? c.variant : 0;
+    L.variant = (c.output == MTB_OUT_TOPK_PHASE || c.output == MTB_OUT_PHASE) ? c.variant : 0;
     if (L.detrend == kDetrendIir) {
         // L/WaveSpecZZ_1.0.2.mq5:3041-3043, same double expressions as the CPU path
         const double omega = 2.0 * M_PI / c.trend_period;

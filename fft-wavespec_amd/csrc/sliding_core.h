@@ -343,7 +343,8 @@ __global__ __launch_bounds__(seed_nt<LOG2N>()) void slide_seed_kernel(SlideArgs 
 // of fft_lds at N/4 threads), one transform m at a time, every output in natural order to LDS and the band read
 // back: Y_m = FFT_N((x[w0 + i] - L) e^{-j m th i}) as slide_seed_kernel (N >= 1024).
 //
-// Seed chains (round 5): a workgroup seeds G = a.seed_chain consecutive segments -- the first by the FFTs, each next one
+// Seed chains (round 5, wsp_plan_set_variant 6 -- an ablation, slower than the default one FFT seed per segment:
+// the chain's slide steps are serial, r05g): a workgroup seeds G = a.seed_chain consecutive segments -- the first by the FFTs, each next one
 // by sliding the band's trackers a.seg windows on from the previous (slide_step, the uniforms of stage_uniforms: the
 // same operations the scan kernel applies, so a chained seed is exactly what the scan wave of the previous segment
 // holds after sliding across the seam, as if the segments were one).  The segment count of the scan (one wave per

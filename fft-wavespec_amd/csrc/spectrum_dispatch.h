@@ -93,9 +93,7 @@ template <typename T, int LOG2N, int DETREND, int OUT> constexpr int default_var
         return (DETREND == kDetrendNone && (LOG2N == 11 || LOG2N == 12)) ? kDefaultVar
                : OUT == kOutTopK                                          ? kCommonVar
                                                                           : (kVarNoPrefetch | kVarNtStore);
-    // (phase record: the split form at N = 2048 / 4096 without the IIR staging, round 5; wsp_plan_set_variant 1 = AoS)
-    if constexpr (OUT == kOutPhase)
-        return ((LOG2N == 11 || LOG2N == 12) && DETREND != kDetrendIir) ? kDefaultVar : (kVarNoPrefetch | kVarNtStore);
+    // (phase record: the AoS form; the split form, wsp_plan_set_variant 2, measured slower, round 5)
     return (OUT == kOutPhase) ? (kVarNoPrefetch | kVarNtStore)
            : (DETREND == kDetrendIir || OUT != kOutPower || (sizeof(T) == 4 && DETREND == kDetrendMean) || LOG2N > 12)
                ? kCommonVar
@@ -153,14 +151,15 @@ hipError_t dispatch_win(const SpectrumLaunch &L, hipStream_t s) {
             }
         }
     }
-    if constexpr (OUT == kOutPhase && (default_var<T, LOG2N, DETREND, OUT>() & kVarSplitLds) != 0) {
-        if (L.variant == 1) {  // the AoS phase record (round 1-4 form, A/B)
-            constexpr int kAos = kVarNoPrefetch | kVarNtStore;
+    // the split-exchange phase record (round 5, wsp_plan_set_variant 2 at N = 2048 / 4096 without IIR): 3 waves per
+    // SIMD, but 1.36 against 1.15 ms for the AoS form at the north star (r05g) -- an ablation, not the default
+    if constexpr (OUT == kOutPhase && (LOG2N == 11 || LOG2N == 12) && DETREND != kDetrendIir) {
+        if (L.variant == 2) {
             switch (window_class(L.window, &a0, &a1, &a2)) {
-            case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos, kAos>(L, s);
-            case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2, kAos>(L, s);
-            case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett, kAos>(L, s);
-            default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone, kAos>(L, s);
+            case kWinCos: return launch_one<T, LOG2N, DETREND, OUT, kWinCos, kDefaultVar>(L, s);
+            case kWinCos2: return launch_one<T, LOG2N, DETREND, OUT, kWinCos2, kDefaultVar>(L, s);
+            case kWinBartlett: return launch_one<T, LOG2N, DETREND, OUT, kWinBartlett, kDefaultVar>(L, s);
+            default: return launch_one<T, LOG2N, DETREND, OUT, kWinNone, kDefaultVar>(L, s);
             }
         }
     }

@@ -323,7 +323,9 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
  *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch; 0 = the
  *    probe-threshold scan (16 windows per batch, 4 waves per SIMD), 4 / 5 = the
- *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave);
+ *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave); 6 =
+ *    the default scan with seed chains (one FFT seed per <= 256 windows, the
+ *    next segments' seeds by sliding the band on; slower, round 5);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams (a one-window
  *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused
@@ -341,8 +343,8 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  *    with the AoS exchange; 3 = 0 with the element loads in natural order
  *    (round 4); 0 = the pre-step in registers, split exchange, each element's
  *    two reads (as X_k and as a mirror X_(M-k)) one load step apart;
- *  - MTB_OUT_PHASE records at N = 2048 / 4096 without IIR detrend: 1 = the
- *    AoS form (two waves per SIMD) instead of the split-exchange form (round 5);
+ *  - MTB_OUT_PHASE records at N = 2048 / 4096 without IIR detrend: 2 = the
+ *    split-exchange form (3 waves per SIMD; slower than the default AoS form);
  *  - MTB_OUT_TOPK_PHASE records (FFT kernel): 1 = the AoS form (two waves per
  *    SIMD, every thread's phase chunk) instead of the split-exchange one-wave
  *    scan + one-wave winners' phases. */

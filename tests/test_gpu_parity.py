@@ -267,11 +267,12 @@ def _topk_match(got, want, tol, full_max):
                                                    ("mean", "hamming", "37"), ("none", "none", "n+5"),
                                                    ("mean", "bartlett", "n/4")])
 def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
-    """Round 5: the split-exchange phase record (default at N = 2048 / 4096 without IIR: Re and Im of X staged
-    through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with its
-    coefficients in SGPRs -- 3 waves per SIMD) against the AoS form (wsp_plan_set_variant 1) and the oracle, over
-    every window: power rows to 1e-13 of each other (the forms evaluate the cosine windows differently)
-    and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of test_phase_output."""
+    """Round 5: the split-exchange phase record (wsp_plan_set_variant 2 at N = 2048 / 4096 without IIR: Re and Im of X
+    staged through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with
+    its coefficients in SGPRs -- 3 waves per SIMD; an ablation, slower than the default) against the AoS form (the
+    default) and the oracle, over every window: power rows to 1e-13 of each other (the forms evaluate the cosine
+    windows differently) and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of
+    test_phase_output."""
     torch = pytest.importorskip("torch")
     hop = {"1": 1, "37": 37, "n/4": n // 4, "n": n, "n+5": n + 5}[hop_of]
     nwin = 90
@@ -279,7 +280,7 @@ def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
     dev = torch.device("cuda", 0)
     d_s = torch.from_numpy(s).to(dev)
     outs = []
-    for v in (0, 1):
+    for v in (2, 0):
         plan = bridge.Plan(0, n, hop, nwin, detrend, window, output="phase")
         plan.set_variant(v)
         d_o = torch.full((nwin * 3 * (n // 2),), float("nan"), dtype=torch.float64, device=dev)
@@ -473,11 +474,12 @@ def test_phase_output(gpu_session, n, detrend, period):
                                                    ("mean", "hamming", "37"), ("none", "none", "n+5"),
                                                    ("mean", "bartlett", "n/4")])
 def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
-    """Round 5: the split-exchange phase record (default at N = 2048 / 4096 without IIR: Re and Im of X staged
-    through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with its
-    coefficients in SGPRs -- 3 waves per SIMD) against the AoS form (wsp_plan_set_variant 1) and the oracle, over
-    every window: power rows to 1e-13 of each other (the forms evaluate the cosine windows differently)
-    and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of test_phase_output."""
+    """Round 5: the split-exchange phase record (wsp_plan_set_variant 2 at N = 2048 / 4096 without IIR: Re and Im of X
+    staged through the 17 KiB split slot one after the other, the three rows written one after another, atan2 with
+    its coefficients in SGPRs -- 3 waves per SIMD; an ablation, slower than the default) against the AoS form (the
+    default) and the oracle, over every window: power rows to 1e-13 of each other (the forms evaluate the cosine
+    windows differently) and both to the oracle's 1e-10; phases and delays by the unwrap / delay bars of
+    test_phase_output."""
     torch = pytest.importorskip("torch")
     hop = {"1": 1, "37": 37, "n/4": n // 4, "n": n, "n+5": n + 5}[hop_of]
     nwin = 90
@@ -485,7 +487,7 @@ def test_phase_split_form(gpu_session, n, detrend, window, hop_of):
     dev = torch.device("cuda", 0)
     d_s = torch.from_numpy(s).to(dev)
     outs = []
-    for v in (0, 1):
+    for v in (2, 0):
         plan = bridge.Plan(0, n, hop, nwin, detrend, window, output="phase")
         plan.set_variant(v)
         d_o = torch.full((nwin * 3 * (n // 2),), float("nan"), dtype=torch.float64, device=dev)

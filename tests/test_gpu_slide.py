@@ -271,11 +271,11 @@ def test_slide_topk_scan_forms_identical(gpu_session, n, pmin, pmax, seg):
                                                       (2048, "mean", "hamming", 7, 3001), (1024, "none", "blackman", 64, 4099),
                                                       (4096, "mean", "hann", 100, 2999), (2048, "none", "none", 2048, 4100)])
 def test_slide_topk_seed_chains(gpu_session, n, detrend, window, seg, nwin):
-    """Round 5: the top-k seeds in chains (one FFT seed per chain of <= 256 windows, the next segments' seeds by
-    sliding the band's trackers on, wsp_plan_set_variant 6 = one FFT seed per segment): against the unchained form and
-    the oracle on every window -- the policy's segments of a one-eighth C4 shard (131072 windows: chains of 5 segments of
-    64), short segments (chains of 16 x 7 windows, the chain cap), a ragged last chain, the mean detrend (the chain's
-    level L carried in the seed record) and a segment too long to chain."""
+    """Round 5: the top-k seeds in chains (wsp_plan_set_variant 6, an ablation: one FFT seed per chain of <= 256
+    windows, the next segments' seeds by sliding the band's trackers on; the default seeds every segment by FFTs):
+    against the unchained form and the oracle on every window -- the policy's segments of a one-eighth C4 shard (131072
+    windows: chains of 5 segments of 64), short segments (chains of 16 x 7 windows, the chain cap), a ragged last
+    chain, the mean detrend (the chain's level L carried in the seed record) and a segment too long to chain."""
     torch = pytest.importorskip("torch")
     s = synth.random_walk(nwin + n - 1, seed=n + seg + 5)
     outs = []
@@ -288,7 +288,7 @@ def test_slide_topk_seed_chains(gpu_session, n, detrend, window, seg, nwin):
             plan.set_slide_segment(seg)
         outs.append(_run(plan, s, torch).reshape(nwin, 8, 4))
         plan.close()
-    chained, single = outs
+    single, chained = outs
     same = chained[:, :, 0] == single[:, :, 0]
     assert (~same).sum() <= 8
     if nwin > 20000:  # the full shard: the oracle on a spread of windows (every 64-window segment seam near 0 / mid / end)
