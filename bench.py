@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--algo", default="auto", choices=["auto", "fft", "slide"],
                     help="hop = 1 power batches: seeded sliding DFT or FFT per window (wsp_plan_set_algorithm)")
     ap.add_argument("--slide-seg", type=int, default=0, help="windows per sliding-DFT workgroup (0 = library policy)")
+    ap.add_argument("--seed-chain", type=int, default=0,
+                    help="hop = 1 top-k: segments per seed workgroup (wsp_plan_set_seed_chain; 0 = library policy)")
     ap.add_argument("--variant", type=int, default=0, help="kernel form (wsp_plan_set_variant; ablations)")
     ap.add_argument("--chunk", type=int, default=0, help="windows per chunk of the two-pass large-N path (wsp_plan_set_chunk)")
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
@@ -350,7 +352,8 @@ def shard_plan(name: str, rank: int, world: int, scaling: str, c5_shard: str = "
 class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
-    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0, chunk=0):
+    def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0, chunk=0,
+                 seed_chain=0):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -386,6 +389,8 @@ class SingleBatch(Workload):
                 self.plan.set_slide_segment(slide_seg)
             if variant:
                 self.plan.set_variant(variant)
+            if seed_chain:
+                self.plan.set_seed_chain(seed_chain)
             if chunk:
                 self.plan.set_chunk(chunk)
         self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
@@ -579,7 +584,7 @@ def main(argv=None):
                      args.c5_streams, args.c5_mode, args.c5_shard)
     else:
         wl = SingleBatch(args.config, shard_rank, local_rank, shard_world, scaling, args.algo, args.slide_seg,
-                         args.variant, args.chunk)
+                         args.variant, args.chunk, args.seed_chain)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)

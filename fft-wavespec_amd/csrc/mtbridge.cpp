@@ -308,6 +308,7 @@ struct Config {
     int topk = 0, kmin = 0, kmax = -1;  // MTB_OUT_TOPK / MTB_OUT_TOPK_PHASE
     int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
     int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
+    int seed_chain = 0;                 // top-k segments per seed workgroup, 0 = auto (wsp_plan_set_seed_chain)
     int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
     unsigned char *scan_flags = nullptr;  // wsp_plan_set_scan_flags: per-window path of the probe-threshold top-k scan
     int64_t chunk = 0;                  // N > 16384 two-pass path: windows per chunk, 0 = large_chunk (wsp_plan_set_chunk)
@@ -587,7 +588,9 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             // variant 6 (ablation): seed chains of <= 256 windows -- one FFT seed per chain, the next segments' seeds
             // by sliding the band on; slower than one FFT seed per segment (C4 top-8 0.404 against 0.355 ms, a 1/8
             // shard 0.113 against 0.096, r05g: the chain's serial slide steps outlast the parallel FFT seeds)
-            A.seed_chain = c.variant == 6 ? (int)std::min<int64_t>(16, 1 + 256 / A.seg) : 1;
+            // (wsp_plan_set_seed_chain sets the length; a chain's slide is staged in LDS, <= 256 steps)
+            const int cap = (int)std::min<int64_t>(16, 1 + 256 / A.seg);
+            A.seed_chain = c.seed_chain > 0 ? std::min(cap, c.seed_chain) : (c.variant == 6 ? cap : 1);
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }
@@ -2032,6 +2035,17 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows) {
     const int sw = plan_ws_fit(*p);
     if (sw != MTB_OK) p->cfg = old;
     return sw;
+}
+
+MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || segments < 0 || segments > 16) {
+        set_error("wsp_plan_set_seed_chain(%lld, %d): unknown plan or chain outside 0..16", (long long)plan, segments);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.seed_chain = segments;
+    return MTB_OK;
 }
 
 MTB_API int32_t wsp_plan_set_chunk(int64_t plan, int64_t windows) {

@@ -317,6 +317,13 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
  * number of slides, so at most 2048 (the longest length the parity tests
  * cover); MTB_BAD_ARGS for an unknown plan or windows outside 0..2048. */
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
+/* Tuning (hop = 1 top-k records, N >= 1024): segments per seed workgroup.  The
+ * first segment of a chain is seeded by the FFTs, each next one by sliding the
+ * band's trackers on from the previous (the scan's own operations, so the
+ * records are identical); 1 = one FFT seed per segment, 0 = the library's
+ * policy.  Capped at 1 + 256 / segment (a chain's steps are staged in LDS).
+ * MTB_BAD_ARGS for an unknown plan or segments outside 0..16. */
+MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
 /* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import subprocess
 import sys
 import time
@@ -44,15 +45,15 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--extra", default="", help="extra bench.py arguments, comma-separated")
     a = ap.parse_args()
-    gs = [int(g) for g in a.gpus.split(",")]
+    gs = [int(g) for g in re.split("[,+]", a.gpus)]
     extra = [x for x in a.extra.split(",") if x]
     common = ["--steps", str(a.steps), "--warmup", str(a.warmup)] + extra
     res = {"caveat": "single-GPU emulation, not a scaling curve: each rank's strong-scaling shard is timed alone on "
                      "one MI355X (bench.py --emulate-shard R/G); predicted speed-up = T(whole batch on 1 GPU) / "
                      "max over ranks of T(shard)",
            "steps": a.steps, "warmup": a.warmup, "configs": {}}
-    for cfg in a.configs.split(","):
-        modes = a.c5_shards.split(",") if cfg == "c5" else ["windows"]
+    for cfg in re.split("[,+]", a.configs):
+        modes = re.split("[,+]", a.c5_shards) if cfg == "c5" else ["windows"]
         one = run_bench(["--config", cfg] + common, 300)
         t1 = one["ms_per_step"]
         print(f"{cfg} G=1: {t1:.4f} ms ({one['value']:.4g} windows/s, frac {one['roofline']['frac']:.3f})", flush=True)

@@ -306,6 +306,31 @@ def test_slide_topk_seed_chains(gpu_session, n, detrend, window, seg, nwin):
         _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
 
 
+@pytest.mark.parametrize("seg,chain", [(32, 2), (32, 3), (64, 2), (48, 4), (40, 16)])
+def test_slide_topk_seed_chain_lengths(gpu_session, seg, chain):
+    """wsp_plan_set_seed_chain: chains of an explicit length (the shard policy's short segments, two to four per
+    chain; 16 is capped to 1 + 256 / seg) against one FFT seed per segment and the oracle on every window."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 2048, 5000
+    s = synth.random_walk(nwin + n - 1, seed=seg * 31 + chain)
+    outs = []
+    for c in (1, chain):
+        plan = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+        plan.set_topk(8, 18.0, 200.0)
+        plan.set_algorithm("slide")
+        plan.set_slide_segment(seg)
+        plan.set_seed_chain(c)
+        outs.append(_run(plan, s, torch).reshape(nwin, 8, 4))
+        plan.close()
+    single, chained = outs
+    assert ((chained[:, :, 0] != single[:, :, 0]).sum()) <= 8
+    want = oracle.batch_topk(s, n, 1, "none", "hann", 0, None, 8, 18.0, 200.0)
+    spec = oracle.batch_spectrum(s, n, 1, "none", "hann")
+    kmin, kmax = oracle.band(n)
+    for got in outs:
+        _topk_bars(got, want, spec[:, kmin:kmax + 1].max(axis=1), max_swaps=4)
+
+
 @pytest.mark.parametrize("case", ["zeros", "ones_mean", "zeros_then_walk"])
 def test_slide_topk_exact_ties(gpu_session, case):
     """Exactly tied band powers: a zero series (every tracker stays exactly 0), a constant 1.0 with
