@@ -1224,6 +1224,10 @@ struct Group {
     int mode = 0;
     int *ctr = nullptr;                    // 256 task-counter slots (counter, done) on the device, zeroed at create
     uint32_t exec_no = 0;
+    // per slot: the event its last execute recorded and that execute's stream -- an execute on another stream
+    // waits for the slot's previous user before it reuses the counters (more than 256 executes in flight)
+    std::vector<hipEvent_t> slot_ev;
+    std::vector<hipStream_t> slot_st;
     long long *trace = nullptr;            // wsp_group_set_trace: diagnostic per-task timeline of the mixed launch
     int64_t trace_cap = 0, last_tasks = 0;
     // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
@@ -1246,6 +1250,8 @@ struct Group {
             (void)hipDeviceSynchronize();  // a queued execute may still count on its slot
             (void)hipFree(ctr);
         }
+        for (auto e : slot_ev)
+            if (e) (void)hipEventDestroy(e);
     }
 };
 std::mutex g_groups_mu;
@@ -1343,8 +1349,17 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     const int slot = (int)(g.exec_no++ % kMixSlots);
     m.counter = g.ctr + 2 * slot;
     m.done = g.ctr + 2 * slot + 1;
+    if (g.slot_ev.empty()) {
+        g.slot_ev.assign(kMixSlots, nullptr);
+        g.slot_st.assign(kMixSlots, nullptr);
+    }
+    hipEvent_t &ev = g.slot_ev[slot];
+    if (!ev) HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), MTB_INTERNAL_ERROR);
+    else if (g.slot_st[slot] != s) HIP_OR(hipStreamWaitEvent(s, ev, 0), MTB_INTERNAL_ERROR);  // same stream: in order
     const int grid = (int)std::min<int64_t>(res, tasks);
     HIP_OR(launch_slide_mix(m, nf, det, c0.f32, grid, s), MTB_INTERNAL_ERROR);
+    HIP_OR(hipEventRecord(ev, s), MTB_INTERNAL_ERROR);
+    g.slot_st[slot] = s;
     return MTB_OK;
 }
 

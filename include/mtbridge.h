@@ -395,7 +395,13 @@ MTB_API int64_t wsp_group_create(int32_t device, int32_t n_members, const int32_
  * (events): work enqueued on `hip_stream` after the execute sees every
  * member's output.  The internal streams belong to the group and every execute
  * uses them, so executes of one group issued on different caller streams run
- * one after another, not concurrently (use one group per concurrent caller). */
+ * one after another, not concurrently (use one group per concurrent caller).
+ * The mixed-length launch (the default mode) uses no internal streams and
+ * ignores wsp_group_set_streams: it runs on `hip_stream` alone, so executes of
+ * one group on different caller streams DO run concurrently -- each takes one
+ * of 256 device task-counter slots in turn, and an execute whose slot's
+ * previous user ran on another stream waits for it (an event) before reusing
+ * the slot, so any number may be in flight. */
 MTB_API int32_t wsp_group_execute(int64_t group, const void *const *d_series, void *const *d_out, void *hip_stream);
 /* Algorithmic bytes of one execute (sum over members, as wsp_plan_algorithmic_bytes). */
 MTB_API int64_t wsp_group_algorithmic_bytes(int64_t group);
