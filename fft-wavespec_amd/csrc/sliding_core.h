@@ -443,8 +443,11 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     for (int g = 1; g < chain; ++g) {
         const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
         if (wsg0 > nsteps) break;
-#pragma unroll 1
-        for (int64_t st = wsg0 - seg; st < wsg0; ++st) slide_step<JB, NF, DETREND>(trk, om, u + st * REC, sum);
+        // unrolled: the LDS reads of 8 steps' uniforms issue together, ahead of the dependent tracker updates
+        // (one read + wait per step put the LDS latency on every step of the serial chain)
+        const int st1 = (int)wsg0;
+#pragma unroll 8
+        for (int st = st1 - (int)seg; st < st1; ++st) slide_step<JB, NF, DETREND>(trk, om, u + st * REC, sum);
         d2 *__restrict__ wsg = ws + g * stride;
 #pragma unroll
         for (int i = 0; i < JB; ++i) {

@@ -128,7 +128,9 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, 2) void inverse_kernel(const dou
 // X_k (once as k, once as the partner's mirror) fall one load step apart instead of up to 15, and the second one
 // hits the line the first brought into L2 (in natural order 0.3 of the second reads went to HBM: PMC 2.79 GB of
 // reads per step against 2.15 GB algorithmic, profiles/r04/inverse_*); variant 3 keeps the natural order.
-template <int LOG2N, int SPLIT, bool PAIRED = true>
+// NTS: non-temporal sample stores (the default); variant 4 = plain stores (a pure write stream ran 5.75 TB/s with
+// plain 16-B stores against 5.5 with non-temporal ones, profiles/r02/slide/write_probe.log).
+template <int LOG2N, int SPLIT, bool PAIRED = true, bool NTS = true>
 __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_direct_kernel(
     const double *__restrict__ in, double *__restrict__ out, const cpx<double> *__restrict__ tw, int64_t n_windows,
     int64_t n_groups) {
@@ -193,10 +195,15 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_dire
             T *xo = out + w * N;
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
-                __builtin_nontemporal_store(v2{u0[r].re * kScale, -u0[r].im * kScale},
-                                            reinterpret_cast<v2 *>(xo + 2 * (bq0 + B * r)));
-                __builtin_nontemporal_store(v2{u1[r].re * kScale, -u1[r].im * kScale},
-                                            reinterpret_cast<v2 *>(xo + 2 * (bq1 + B * r)));
+                const v2 a = {u0[r].re * kScale, -u0[r].im * kScale}, b = {u1[r].re * kScale, -u1[r].im * kScale};
+                v2 *pa = reinterpret_cast<v2 *>(xo + 2 * (bq0 + B * r)), *pb = reinterpret_cast<v2 *>(xo + 2 * (bq1 + B * r));
+                if constexpr (NTS) {
+                    __builtin_nontemporal_store(a, pa);
+                    __builtin_nontemporal_store(b, pb);
+                } else {
+                    *pa = a;
+                    *pb = b;
+                }
             }
         }
     }
@@ -271,7 +278,8 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
     const auto *tw = static_cast<const cpx<double> *>(L.twiddle);
     // the C2R pre-step in registers with the split exchange at N = 2048 .. 8192 (inverse_direct_kernel); variant 1
     // = the LDS pre-step kernel (round 1-3 form), variant 2 = the register pre-step with the AoS exchange, variant 3 =
-    // the element loads in natural order (round 4; the default pairs each element's two reads in time)
+    // the element loads in natural order (round 4; the default pairs each element's two reads in time), variant 4 = plain
+    // sample stores
 #define INV_CASE(LG)                                                                                          \
     case LG: {                                                                                                \
         const int64_t groups = (L.n_windows + Geo<LG>::WPB - 1) / Geo<LG>::WPB;                               \
@@ -286,6 +294,9 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
         else if (L.variant == 3)                                                                              \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, false>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, \
                                L.in, L.out, tw, L.n_windows, groups);                                         \
+        else if (L.variant == 4)                                                                              \
+            hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, true, false>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, \
+                               stream, L.in, L.out, tw, L.n_windows, groups);                                 \
         else                                                                                                  \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 2>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
                                L.out, tw, L.n_windows, groups);                                               \

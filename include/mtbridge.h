@@ -348,8 +348,9 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
  *    with the AoS exchange; 3 = 0 with the element loads in natural order
- *    (round 4); 0 = the pre-step in registers, split exchange, each element's
- *    two reads (as X_k and as a mirror X_(M-k)) one load step apart;
+ *    (round 4); 4 = 0 with plain (not non-temporal) sample stores; 0 = the
+ *    pre-step in registers, split exchange, each element's two reads (as X_k
+ *    and as a mirror X_(M-k)) one load step apart;
  *  - MTB_OUT_PHASE records at N = 2048 / 4096 without IIR detrend: 2 = the
  *    split-exchange form (3 waves per SIMD; slower than the default AoS form);
  *  - MTB_OUT_TOPK_PHASE records (FFT kernel): 1 = the AoS form (two waves per
