@@ -309,6 +309,8 @@ struct Config {
     int algo = MTB_ALGO_AUTO;           // wsp_plan_set_algorithm
     int64_t slide_seg = 0;              // windows per sliding-DFT workgroup, 0 = auto (wsp_plan_set_slide_segment)
     int seed_chain = 0;                 // top-k segments per seed workgroup, 0 = auto (wsp_plan_set_seed_chain)
+    long long *trace = nullptr;         // diagnostic timeline of the hop = 1 top-k kernels (wsp_plan_set_trace)
+    int64_t trace_cap = 0;
     int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
     unsigned char *scan_flags = nullptr;  // wsp_plan_set_scan_flags: per-window path of the probe-threshold top-k scan
     int64_t chunk = 0;                  // N > 16384 two-pass path: windows per chunk, 0 = large_chunk (wsp_plan_set_chunk)
@@ -591,6 +593,8 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             // (wsp_plan_set_seed_chain sets the length; a chain's slide is staged in LDS, <= 256 steps)
             const int cap = (int)std::min<int64_t>(16, 1 + 256 / A.seg);
             A.seed_chain = c.seed_chain > 0 ? std::min(cap, c.seed_chain) : (c.variant == 6 ? cap : 1);
+            A.trace = c.trace;
+            A.trace_cap = c.trace_cap;
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }
@@ -2015,9 +2019,9 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 9;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..8", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..9", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);
@@ -2060,6 +2064,18 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments) {
     }
     std::lock_guard<std::mutex> lk(p->mu);
     p->cfg.seed_chain = segments;
+    return MTB_OK;
+}
+
+MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || capacity < 0 || (capacity > 0 && !d_trace)) {
+        set_error("wsp_plan_set_trace(%lld): unknown plan or null buffer", (long long)plan);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.trace = capacity > 0 ? static_cast<long long *>(d_trace) : nullptr;
+    p->cfg.trace_cap = capacity;
     return MTB_OK;
 }
 

@@ -363,6 +363,14 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     const int64_t sg0 = (int64_t)blockIdx.x * chain;  // this workgroup's first segment
     const int64_t w0 = sg0 * a.seg;
     if (w0 >= a.n_windows) return;
+    // diagnostic timeline (wsp_plan_set_trace): [workgroup | XCC << 32, start, FFT 0 done, seeds done, chain done, end]
+    long long *trc = a.trace && 6 * ((int64_t)blockIdx.x + 1) <= a.trace_cap / 2 && t == 0 ? a.trace + 6 * (int64_t)blockIdx.x : nullptr;
+    if (trc) {
+        unsigned xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        trc[0] = (long long)blockIdx.x | ((long long)(xcc & 15) << 32);
+        trc[1] = wall_clock64();
+    }
     const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
     const core::cpx<double> *__restrict__ tw = static_cast<const core::cpx<double> *>(a.twiddle);
     const d2 *__restrict__ mod = static_cast<const d2 *>(a.omega) + (NF + 1) * M;  // [NM][N] e^{-j m th i}
@@ -417,8 +425,12 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             if (t == 0) ws[NF * span] = d2{sum, lvl};  // and L
         }
         __syncthreads();  // the band reads before the next transform's exchanges
+        if (trc) trc[2 + (m > 0)] = wall_clock64();
     }
-    if (chain == 1) return;
+    if (chain == 1) {
+        if (trc) trc[4] = trc[5] = wall_clock64();
+        return;
+    }
     d2 om[JB][NF];
     const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
 #pragma unroll
@@ -458,6 +470,7 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
         }
         if (t == 0) wsg[NF * span] = d2{sum, lvl};  // the chain's level L (the scan's uniforms follow x - L)
     }
+    if (trc) trc[4] = trc[5] = wall_clock64();
 }
 
 // One wave per segment: lane l tracks bins kmin + l + 64 b (b < NB), stages each window's band X in LDS
@@ -769,6 +782,11 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
     const int l = threadIdx.x;
     const int64_t w0 = (int64_t)blockIdx.x * a.seg;
     if (w0 >= a.n_windows) return;
+    // diagnostic timeline (wsp_plan_set_trace): [start, end] of this workgroup
+    long long *trs = a.trace && a.trace_cap / 2 + 2 * ((int64_t)blockIdx.x + 1) <= a.trace_cap && l == 0
+                         ? a.trace + a.trace_cap / 2 + 2 * (int64_t)blockIdx.x
+                         : nullptr;
+    if (trs) trs[0] = wall_clock64();
     const int len = (int)((a.n_windows - w0) < a.seg ? (a.n_windows - w0) : a.seg);
     const double *__restrict__ x = static_cast<const double *>(a.series) + w0;
     const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);
@@ -902,6 +920,7 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
             }
         }
     }
+    if (trs) trs[1] = wall_clock64();
 }
 
 template <int LOG2N, int NF, int DETREND> hipError_t launch_topk_t(const SlideArgs &a, hipStream_t s) {

@@ -137,6 +137,8 @@ struct SlideArgs {
                           // segments fill 1/share of the resident workgroup slots; 0 / 1 = all of them
     int seed_chain;       // top-k seeds (N >= 1024): segments per seed workgroup -- one FFT seed, the next ones by
                           // sliding the band's trackers seg windows at a time (<= 1: one FFT seed per segment)
+    long long *trace;     // diagnostic (wsp_plan_set_trace): top-k seed workgroup b writes 6 ticks at 6 b, scan workgroup
+    int64_t trace_cap;    // b 2 ticks at trace_cap / 2 + 2 b, while they fit in trace_cap int64 entries; nullptr = off
 };
 hipError_t launch_slide(const SlideArgs &a, hipStream_t stream);
 // Grouped launch: several series of the same window length (the symbols of one length in a

@@ -69,6 +69,7 @@ SIGNATURES = {
     "wsp_plan_get_algorithm": (C.c_int32, [C.c_int64]),
     "wsp_plan_set_slide_segment": (C.c_int32, [C.c_int64, C.c_int64]),
     "wsp_plan_set_seed_chain": (C.c_int32, [C.c_int64, C.c_int32]),
+    "wsp_plan_set_trace": (C.c_int32, [C.c_int64, C.c_void_p, C.c_int64]),
     "wsp_plan_set_variant": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_set_scan_flags": (C.c_int32, [C.c_int64, C.c_void_p]),
     "wsp_plan_set_chunk": (C.c_int32, [C.c_int64, C.c_int64]),
@@ -334,6 +335,10 @@ class Plan:
     def set_seed_chain(self, segments: int) -> None:
         """Tuning: top-k segments per seed workgroup (1 = one FFT seed each, 0 = the library's policy)."""
         _check("wsp_plan_set_seed_chain", lib().wsp_plan_set_seed_chain(self.handle, segments))
+
+    def set_trace(self, d_trace: int, capacity: int) -> None:
+        """Diagnostic: timeline of the hop = 1 top-k kernels into a device buffer of `capacity` int64."""
+        _check("wsp_plan_set_trace", lib().wsp_plan_set_trace(self.handle, d_trace, capacity))
 
     def set_variant(self, variant: int) -> None:
         """Ablation: the kernel form (include/mtbridge.h wsp_plan_set_variant; 0 = the library's choice)."""

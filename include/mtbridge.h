@@ -324,7 +324,14 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  * policy.  Capped at 1 + 256 / segment (a chain's steps are staged in LDS).
  * MTB_BAD_ARGS for an unknown plan or segments outside 0..16. */
 MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
-/* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
+/* Diagnostic: a timeline of the hop = 1 top-k kernels of later executes into
+ * d_trace, a device buffer of `capacity` int64 (wall-clock ticks, 100 MHz):
+ * seed workgroup b writes [b | XCC << 32, start, FFT m = 0 done, seeds done,
+ * chain done, end] at 6 b and scan workgroup b [start, end] at capacity / 2 +
+ * 2 b, each while it fits.  capacity = 0 turns it off (the default).
+ * MTB_BAD_ARGS for an unknown plan or a null buffer. */
+MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
+/* Tuning / ablation: the kernel form, 0..9 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -342,7 +349,8 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  *    with 16-column column-pass workgroups (the default takes 8); 7 = the
  *    two-pass row kernel in plain block order (the default is XCD-aware);
  *    8 = two passes with 8-column column-pass workgroups at M2 = 256 (fp64
- *    N = 65536 / 131072);
+ *    N = 65536 / 131072); 9 = the fused form with next-block L2 touches
+ *    (fp64 N = 65536);
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
