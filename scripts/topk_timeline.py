@@ -29,7 +29,7 @@ def run(r, g, seg, chain):
     for _ in range(30):
         wl.step()
     torch.cuda.synchronize()
-    cap = 1 << 20
+    cap = 3 << 19  # half for the seed records (6 entries each), half for the scan records (2 each)
     tr = torch.zeros(cap, dtype=torch.int64, device="cuda")
     wl.plan.set_trace(tr.data_ptr(), cap)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -39,7 +39,7 @@ def run(r, g, seg, chain):
     torch.cuda.synchronize()
     wl.plan.set_trace(0, 0)
     t = tr.cpu().numpy()
-    seeds = t[: cap // 2].reshape(-1, 6)
+    seeds = t[: cap // 2 // 6 * 6].reshape(-1, 6)
     seeds = seeds[seeds[:, 1] > 0]
     scans = t[cap // 2:].reshape(-1, 2)
     scans = scans[scans[:, 0] > 0]
