@@ -277,15 +277,8 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // recycled-slot round trip.  Same arithmetic as col_kernel / row_kernel (same wg_fft, twiddles and
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
-//
-// TCH (round 5, variant 9): while a block's FFT runs, every thread touches two 128-B lines of the NEXT block's
-// inputs (the next column block's sample rows, the next row block's slot rows, and in the last row block the next
-// window's first column block) with dword loads whose values are only consumed, by an empty asm, when that block's
-// own loads start: the lines are on their way into L2 during the FFT instead of after it, without the registers a
-// full prefetch needs (PF: ~360 VGPRs, one wave per SIMD) and without LDS (the column exchange fills it).  Plain
-// register loads: a barrier does not wait for them (an LDS-DMA touch would be fenced by every __syncthreads).
 template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true,
-          bool NTS = false, int TCH = 0>
+          bool NTS = false>
 __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
@@ -332,36 +325,6 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) nxt[r] = yr[rt + TPR * r];
     };
-    // touches (TCH): lines of 128 B, LPC per column-block row, LPR per slot row
-    constexpr int LPC = CB * 2 * (int)sizeof(T) / 128, LPR = M1 * 2 * (int)sizeof(T) / 128;
-    static_assert(TCH == 0 || (M2 * LPC == 2 * NT && 2 * RB * LPR == 2 * NT), "two touched lines per thread");
-    float tch0 = 0.f, tch1 = 0.f;
-    auto touch_cols = [&](int64_t wn, int b) {
-        const T *__restrict__ xw = series + wn * a.hop;
-        int l0 = tid;
-        asm volatile("" : "+v"(l0));  // the lane offsets are recomputed per touch, not hoisted and kept live
-        if constexpr (TCH == 1) l0 *= 2;  // one line per thread: every other line of the block
-        const int l1 = l0 + NT;
-        tch0 = *reinterpret_cast<const float *>(xw + 2 * (b * CB + (128 / (2 * (int)sizeof(T))) * (l0 % LPC) + M1 * (l0 / LPC)));
-        if constexpr (TCH == 2)
-            tch1 = *reinterpret_cast<const float *>(xw + 2 * (b * CB + (128 / (2 * (int)sizeof(T))) * (l1 % LPC) + M1 * (l1 / LPC)));
-    };
-    auto touch_rows = [&](int b2) {
-        auto line = [&](int l) {
-            const int sl = l / LPR, il = sl < RB ? sl : sl - RB, lo = b2 * RB + il;
-            const int row = sl < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
-            return reinterpret_cast<const float *>(y + (int64_t)row * M1 + (128 / (2 * (int)sizeof(T))) * (l % LPR));
-        };
-        int l0 = tid;
-        asm volatile("" : "+v"(l0));
-        if constexpr (TCH == 1) l0 *= 2;
-        tch0 = *line(l0);
-        if constexpr (TCH == 2) tch1 = *line(l0 + NT);
-    };
-    auto touched = [&]() {
-        if constexpr (TCH == 2) asm volatile("" ::"v"(tch0), "v"(tch1));
-        else asm volatile("" ::"v"(tch0));
-    };
     // window angle of this thread's first sample pair in column block 0 (th * 2 (cc + M1 ct)), and the
     // rotation by th * 2 CB from one column block to the next (<= NB1 - 1 steps): no sincos in the loop
     double cw00 = 1.0, sw00 = 0.0, cbd = 1.0, sbd = 0.0;
@@ -375,7 +338,6 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
         const double mean = MEAN ? a.means[w] : 0.0;
         double cwb = cw00, swb = sw00;  // angle of column block beta
         for (int beta = 0; beta < NB1; ++beta) {
-            if constexpr (TCH > 0) touched();
             if (!PF) load_cols(w, beta);
             const int n1 = beta * CB + cc;
             double cw = cwb, sw = swb;
@@ -415,9 +377,6 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
             }
             // next block's samples in flight during this FFT (not across the row pass: registers)
             if (PF && beta + 1 < NB1) load_cols(w, beta + 1);
-            if constexpr (TCH > 0) {
-                if (beta + 1 < NB1) touch_cols(w, beta + 1);
-            }
             wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
             constexpr int R = last_radix<LOG2M2>();
             const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
@@ -436,7 +395,6 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
         // ---- row pass: NB2 blocks of RB rows + their mirror rows
         if (PF) load_rows(0);
         for (int beta2 = 0; beta2 < NB2; ++beta2) {
-            if constexpr (TCH > 0) touched();
             if (!PF) load_rows(beta2);
             const int i = rho < RB ? rho : rho - RB, lo = beta2 * RB + i;
             const int row = rho < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
@@ -445,10 +403,6 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = nxt[r];
             if (PF && beta2 + 1 < NB2) load_rows(beta2 + 1);
-            if constexpr (TCH > 0) {
-                if (beta2 + 1 < NB2) touch_rows(beta2 + 1);
-                else if (w + gridDim.x < a.nwin) touch_cols(w + gridDim.x, 0);
-            }
             wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
             constexpr int R = last_radix<LOG2M1>();
 #pragma unroll
@@ -666,7 +620,7 @@ template <typename T, int LM1, int LM2> hipError_t chunk_launch(const LargeLaunc
 
 // the fused form for M2 = 256 (N = 65536, 131072): one launch over every window (ablations: variant 3 =
 // 512 threads without register prefetch, two waves per SIMD; variant 4 = 256 threads with prefetch)
-template <typename T, int LM1, int NT, bool PF, bool NTS = false, int TCH = 0>
+template <typename T, int LM1, int NT, bool PF, bool NTS = false>
 hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const large::RowArgs &ra, int wclass, bool mean,
                         hipStream_t s) {
     large::ColArgs ca = ca0;
@@ -679,11 +633,11 @@ hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const l
     using namespace core;
 #define FUSED(WC)                                                                                                          \
     if (mean) {                                                                                                            \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS, TCH>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF, NTS, TCH>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     } else {                                                                                                               \
-        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF, NTS, TCH>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
-        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF, NTS, TCH>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
+        else hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, false, false, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
     }
     switch (wclass) {
     case kWinCos: FUSED(kWinCos); break;
@@ -812,11 +766,6 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     if ((L.variant == 3 || fused_default) && (log2m == 15 || log2m == 16))
         return log2m == 15 ? fused_launch<T, 7, 512, false, true>(L, ca, ra, wclass, means != nullptr, s)
                            : fused_launch<T, 8, 512, false, true>(L, ca, ra, wclass, means != nullptr, s);
-    if constexpr (sizeof(T) == 8) {
-        if (L.variant == 9 && log2m == 15)  // the fused form with next-block touches (TCH), fp64
-            return L.chunk % 2 ? fused_launch<T, 7, 512, false, true, 1>(L, ca, ra, wclass, means != nullptr, s)
-                               : fused_launch<T, 7, 512, false, true, 2>(L, ca, ra, wclass, means != nullptr, s);
-    }
     if (L.variant == 5 && log2m == 15)  // ablation: the fused form with plain output stores
         return fused_launch<T, 7, 512, false, false>(L, ca, ra, wclass, means != nullptr, s);
     if (L.variant == 4 && (log2m == 15 || log2m == 16))

@@ -331,7 +331,7 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  * 2 b, each while it fits.  capacity = 0 turns it off (the default).
  * MTB_BAD_ARGS for an unknown plan or a null buffer. */
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
-/* Tuning / ablation: the kernel form, 0..9 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -349,8 +349,7 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    with 16-column column-pass workgroups (the default takes 8); 7 = the
  *    two-pass row kernel in plain block order (the default is XCD-aware);
  *    8 = two passes with 8-column column-pass workgroups at M2 = 256 (fp64
- *    N = 65536 / 131072); 9 = the fused form with next-block L2 touches
- *    (fp64 N = 65536);
+ *    N = 65536 / 131072);
  *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
  *    one-lane-per-window filter;
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
