@@ -1292,41 +1292,19 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     int64_t S = g.seg;
     const bool policy = S <= 0;
     bool above_floor = false;
-    // small batches (fewer than two tasks per resident workgroup at the floor -- a strong-scaled shard): one task per
-    // CU, every task the same length -- S_c windows per segment with S_c x (bins per thread of class c) equal across
-    // the classes, sized so the tasks just cover the CUs.  A 1/8 C5 shard at the floor's 128 windows had 220-395
-    // tasks of two costs (a 2048-point task = two segments x 1024 bins, a 1024-point task half of it), so the rank
-    // waited for its few long tasks while co-running short ones on the same CUs (timeline r05m: busy 0.56 on the
-    // rank with both classes).  Class geometry: P sub-workgroups of N / (2 B) threads, B bins per thread.
-    std::vector<int64_t> small_seg;  // per distinct length, longest first; empty = the regular policy
+    // small batches (fewer than two tasks per resident workgroup at the floor -- a strong-scaled shard): every task the
+    // same length.  A task of the N <= 1024 classes holds half the bins of a 2048 / 4096 task at the same segment length
+    // (B = bsmall bins per thread instead of 4), so those classes take segments 4 / B times as long.  A 1/8 C5 shard
+    // holding 2048- and 1024-point windows at one length had 395 tasks of two costs: the rank waited for its long
+    // tasks while short ones doubled up on their CUs (r05m timeline: busy 0.56; 0.133-0.141 ms against 0.109-0.116
+    // for the single-length ranks).  Measured and dropped (r05n): one task per CU at segments just covering the CUs
+    // (S = 110 instead of 128 on a 2048-point shard) -- every rank 4-10 % slower: the shard's slide is bound by the
+    // aggregate write rate, not by idle CUs, and the extra seeds cost more.
+    bool small = false;
     if (policy) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
         above_floor = S > 128;
-        if (!above_floor && g.mode == 0) {
-            const int cus = cu_count(g.dev);
-            std::vector<std::pair<int, int64_t>> cls;  // (log2n, windows), longest first
-            for (int i = 0; i < n; ++i) {
-                const Config &c = g.cfg[order[i]];
-                if (cls.empty() || cls.back().first != c.log2n) cls.push_back({c.log2n, 0});
-                cls.back().second += c.n_windows;
-            }
-            auto bpt = [&](int l2) { return l2 <= 10 ? (int)m.bsmall : 4; };
-            auto subs = [&](int l2) { return kMixNT * 2 * bpt(l2) / (1 << l2); };
-            double q = 0.0;  // segment steps x bins per thread of every task
-            for (auto &c : cls) q += (double)c.second * bpt(c.first) / subs(c.first);
-            q /= cus;
-            for (int it = 0; it < 64; ++it) {  // rounding: grow q until the tasks fit the CUs
-                int64_t tk = 0;
-                small_seg.clear();
-                for (auto &c : cls) {
-                    const int64_t sc = std::max<int64_t>(32, (int64_t)std::ceil(q / bpt(c.first)));
-                    small_seg.push_back(sc);
-                    tk += (c.second + sc * subs(c.first) - 1) / (sc * subs(c.first));
-                }
-                if (tk <= cus) break;
-                q *= 1.01;
-            }
-        }
+        small = !above_floor && g.mode == 0;
         S = std::min<int64_t>(256, std::max<int64_t>(128, S));
     }
     // Half-length segments for the last class (the shortest windows, picked up last, drain the launch) when the
@@ -1359,8 +1337,8 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
             SlideArgs A{};
             if ((st = slide_args(g.dev, c, &A)) != MTB_OK) return st;
             m.log2n[nc] = c.log2n;
-            m.seg[nc] = !small_seg.empty() ? (int)small_seg[nc]
-                                           : (int)(tail_half && c.log2n == last_l2 ? std::max<int64_t>(64, S / 2) : S);
+            m.seg[nc] = small && c.log2n <= 10 ? (int)(S * 4 / m.bsmall)
+                                               : (int)(tail_half && c.log2n == last_l2 ? std::max<int64_t>(64, S / 2) : S);
             m.mem0[nc] = i;
             m.c1[nc] = A.c1, m.sn1[nc] = A.sn1, m.c2[nc] = A.c2, m.sn2[nc] = A.sn2, m.inv_n[nc] = A.inv_n;
             m.omega[nc] = A.omega;

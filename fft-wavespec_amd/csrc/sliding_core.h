@@ -452,14 +452,7 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     static_assert(256 * REC <= G::SLOT * 2, "a chain's uniforms fit the FFT's LDS");
     stage_uniforms<double, NF, N>(a, x, lvl, 0, nsteps, nsteps + 1, u, t, TP);
     __syncthreads();
-    for (int g = 1; g < chain; ++g) {
-        const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
-        if (wsg0 > nsteps) break;
-        // unrolled: the LDS reads of 8 steps' uniforms issue together, ahead of the dependent tracker updates
-        // (one read + wait per step put the LDS latency on every step of the serial chain)
-        const int st1 = (int)wsg0;
-#pragma unroll 8
-        for (int st = st1 - (int)seg; st < st1; ++st) slide_step<JB, NF, DETREND>(trk, om, u + st * REC, sum);
+    auto put = [&](int g) {
         d2 *__restrict__ wsg = ws + g * stride;
 #pragma unroll
         for (int i = 0; i < JB; ++i) {
@@ -469,6 +462,67 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             for (int f = 0; f < NF; ++f) wsg[f * span + j] = trk[i][f];
         }
         if (t == 0) wsg[NF * span] = d2{sum, lvl};  // the chain's level L (the scan's uniforms follow x - L)
+    };
+    if (a.variant != 6) {
+        // Block form (the default of wsp_plan_set_seed_chain): the slide is linear in the trackers, tr -> om (tr + u), so
+        // seg steps from T give om^seg T + B with B = the same seg steps from zero trackers.  The blocks B_g of the chain's
+        // segments are independent: up to 3 of them slide side by side (3 dependent chains per thread instead of one
+        // chain 3x as long), then T_g = om^seg T_(g-1) + B_g in order.  Rounding differs from the sequential slide
+        // (variant 6) by a few ulps of the trackers.
+        const int ng = (int)std::min<int64_t>(chain - 1, nsteps / seg);  // chained segments with every step in the batch
+        d2 ps[JB][NF];  // om^seg by squaring
+#pragma unroll
+        for (int i = 0; i < JB; ++i)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                d2 r{1.0, 0.0}, b = om[i][f];
+                for (int e = (int)seg; e; e >>= 1) {
+                    if (e & 1) r = cmul(r, b);
+                    b = cmul(b, b);
+                }
+                ps[i][f] = r;
+            }
+        constexpr int GB = 3;
+        for (int g0 = 1; g0 <= ng; g0 += GB) {
+            d2 acc[GB][JB][NF];
+            double sb[GB];
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+                sb[q] = 0.0;
+#pragma unroll
+                for (int i = 0; i < JB; ++i)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) acc[q][i][f] = d2{0.0, 0.0};
+            }
+            const int nb = ng - g0 + 1 < GB ? ng - g0 + 1 : GB;  // wave-uniform
+#pragma unroll 4
+            for (int st = 0; st < (int)seg; ++st)
+#pragma unroll
+                for (int q = 0; q < GB; ++q)
+                    if (q < nb) slide_step<JB, NF, DETREND>(acc[q], om, u + ((g0 + q - 1) * (int)seg + st) * REC, sb[q]);
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+                if (q >= nb) break;
+#pragma unroll
+                for (int i = 0; i < JB; ++i)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) trk[i][f] = cmul(ps[i][f], trk[i][f]) + acc[q][i][f];
+                sum += sb[q];
+                put(g0 + q);
+            }
+        }
+        if (trc) trc[4] = trc[5] = wall_clock64();
+        return;
+    }
+    for (int g = 1; g < chain; ++g) {
+        const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
+        if (wsg0 > nsteps) break;
+        // unrolled: the LDS reads of 8 steps' uniforms issue together, ahead of the dependent tracker updates
+        // (one read + wait per step put the LDS latency on every step of the serial chain)
+        const int st1 = (int)wsg0;
+#pragma unroll 8
+        for (int st = st1 - (int)seg; st < st1; ++st) slide_step<JB, NF, DETREND>(trk, om, u + st * REC, sum);
+        put(g);
     }
     if (trc) trc[4] = trc[5] = wall_clock64();
 }

@@ -155,7 +155,7 @@ int occ_main(int reps) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     for (int round = 0; round < 2; ++round)
-        for (int64_t w : {(int64_t)16384, (int64_t)32768, (int64_t)65536}) {
+        for (int64_t w : {(int64_t)4096, (int64_t)8192, (int64_t)16384, (int64_t)32768, (int64_t)65536}) {
             for (int k = 0; k < 2; ++k) {
                 auto go = [&]() {
                     if (k) launch_pk4<kcore::kPk2Warm>(x, d, n, w, n, kp, 0);
