@@ -349,7 +349,7 @@ bool use_slide_topk(const Config &c);
 // Windows per top-k segment: whole rounds of resident one-wave workgroups (the default probe scan runs 4 per
 // SIMD = 16 per CU) at <= 256 windows each -- C4 (1,048,576 windows): one round of 4096 segments of 256,
 // 0.371-0.374 ms against 0.389 for 128-window segments (two rounds) and 0.41 / 0.50 for 192 / 384
-// (1.33 rounds / a quarter of the slots idle; profiles/r03/s2/topk_seg.log).  At least 64 windows.
+// (1.33 rounds / a quarter of the slots idle; profiles/r03/s2/topk_seg.log).  At least 32 windows (below).
 // CUs of device `dev`, looked up once per device (the segment policy of a plan follows its own GPU, not the
 // calling thread's current one)
 int cu_count(int dev) {
@@ -361,12 +361,24 @@ int cu_count(int dev) {
     cache[dev].store(cus, std::memory_order_relaxed);
     return cus;
 }
+// Below one round of 64-window segments (a strong-scaled shard: 1/8 of C4 is 131072 windows) the segments go down to
+// 32 windows, so the scan still fills the resident slots (4 waves per SIMD instead of 2), and their seeds come in
+// chains (slide_topk_chain): 1/8 C4 top-8 0.0957 ms at 64-window segments, 0.0912 at 32 with one FFT seed each,
+// 0.0773-0.0802 at 32 in chains of 4 (r05k, r05o; chains of 3 / 5 / 6 0.082-0.088 / 0.079-0.082 / 0.085).
 int64_t slide_topk_seg(const Config &c, int dev) {
     if (c.slide_seg > 0) return c.slide_seg;
     const int64_t res = (int64_t)16 * cu_count(dev);
     const int64_t rounds = (c.n_windows + res * 256 - 1) / (res * 256);
     const int64_t seg = (c.n_windows + res * rounds - 1) / (res * rounds);
-    return seg < 64 ? 64 : seg;
+    return seg < 64 ? std::max<int64_t>(32, seg) : seg;
+}
+// segments per seed workgroup when the plan does not set it (wsp_plan_set_seed_chain): chains of ~128 windows at
+// segments of <= 32 (variant 6, the round-5 ablation, chains of <= 256 windows at any length)
+int slide_topk_chain(const Config &c, int64_t seg) {
+    const int cap = (int)std::min<int64_t>(16, 1 + 256 / seg);
+    if (c.seed_chain > 0) return std::min(cap, c.seed_chain);
+    if (c.variant == 6) return cap;
+    return seg <= 32 ? std::min<int>(cap, (int)((128 + seg - 1) / seg)) : 1;
 }
 WsLayout ws_layout(const Config &c, int dev) {
     WsLayout L;
@@ -591,8 +603,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             // by sliding the band on; slower than one FFT seed per segment (C4 top-8 0.404 against 0.355 ms, a 1/8
             // shard 0.113 against 0.096, r05g: the chain's serial slide steps outlast the parallel FFT seeds)
             // (wsp_plan_set_seed_chain sets the length; a chain's slide is staged in LDS, <= 256 steps)
-            const int cap = (int)std::min<int64_t>(16, 1 + 256 / A.seg);
-            A.seed_chain = c.seed_chain > 0 ? std::min(cap, c.seed_chain) : (c.variant == 6 ? cap : 1);
+            A.seed_chain = slide_topk_chain(c, A.seg);
             A.trace = c.trace;
             A.trace_cap = c.trace_cap;
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);

@@ -378,6 +378,15 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     const int64_t stride = slide_topk_seed_stride(NF, a.span);
     d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + sg0 * stride;
     const int span = a.span, kmin = a.kmin;
+    // seed records: non-temporal stores (default) -- every workgroup writes its chain's records at its end, and the
+    // dirty lines a plain store leaves in L2 are written back at the kernel boundary before the scan can start;
+    // variant 7 keeps plain stores
+    const bool nts = a.variant != 7;
+    auto wst = [&](d2 *p, d2 v) {
+        typedef double v2d __attribute__((ext_vector_type(2)));
+        if (nts) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d *>(p));
+        else *p = v;
+    };
     d2 trk[JB][NF];  // the chain's trackers of bins kmin + t + TP i
     double sum = 0.0;
     double xs[16];
@@ -411,18 +420,18 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             const core::cpx<double> yp = lds[core::pad16(k)];
             if (m == 0) {
                 trk[i][0] = s * d2{yp.re, yp.im};
-                ws[j] = trk[i][0];
+                wst(ws + j, trk[i][0]);
             } else {
                 const core::cpx<double> ym = lds[core::pad16((N - k) & (N - 1))];
                 trk[i][2 * m - 1] = s * d2{yp.re, yp.im};
                 trk[i][2 * m] = s * d2{ym.re, -ym.im};
-                ws[(2 * m - 1) * span + j] = trk[i][2 * m - 1];
-                ws[(2 * m) * span + j] = trk[i][2 * m];
+                wst(ws + (2 * m - 1) * span + j, trk[i][2 * m - 1]);
+                wst(ws + (2 * m) * span + j, trk[i][2 * m]);
             }
         }
         if (m == 0) {
             sum = lds[0].re;  // sum of x - L (mean path)
-            if (t == 0) ws[NF * span] = d2{sum, lvl};  // and L
+            if (t == 0) wst(ws + NF * span, d2{sum, lvl});  // and L
         }
         __syncthreads();  // the band reads before the next transform's exchanges
         if (trc) trc[2 + (m > 0)] = wall_clock64();
@@ -459,61 +468,10 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
             const int j = t + TP * i;
             if (j >= span) continue;
 #pragma unroll
-            for (int f = 0; f < NF; ++f) wsg[f * span + j] = trk[i][f];
+            for (int f = 0; f < NF; ++f) wst(wsg + f * span + j, trk[i][f]);
         }
-        if (t == 0) wsg[NF * span] = d2{sum, lvl};  // the chain's level L (the scan's uniforms follow x - L)
+        if (t == 0) wst(wsg + NF * span, d2{sum, lvl});  // the chain's level L (the scan's uniforms follow x - L)
     };
-    if (a.variant != 6) {
-        // Block form (the default of wsp_plan_set_seed_chain): the slide is linear in the trackers, tr -> om (tr + u), so
-        // seg steps from T give om^seg T + B with B = the same seg steps from zero trackers.  The blocks B_g of the chain's
-        // segments are independent: up to 3 of them slide side by side (3 dependent chains per thread instead of one
-        // chain 3x as long), then T_g = om^seg T_(g-1) + B_g in order.  Rounding differs from the sequential slide
-        // (variant 6) by a few ulps of the trackers.
-        const int ng = (int)std::min<int64_t>(chain - 1, nsteps / seg);  // chained segments with every step in the batch
-        d2 ps[JB][NF];  // om^seg by squaring
-#pragma unroll
-        for (int i = 0; i < JB; ++i)
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                d2 r{1.0, 0.0}, b = om[i][f];
-                for (int e = (int)seg; e; e >>= 1) {
-                    if (e & 1) r = cmul(r, b);
-                    b = cmul(b, b);
-                }
-                ps[i][f] = r;
-            }
-        constexpr int GB = 3;
-        for (int g0 = 1; g0 <= ng; g0 += GB) {
-            d2 acc[GB][JB][NF];
-            double sb[GB];
-#pragma unroll
-            for (int q = 0; q < GB; ++q) {
-                sb[q] = 0.0;
-#pragma unroll
-                for (int i = 0; i < JB; ++i)
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) acc[q][i][f] = d2{0.0, 0.0};
-            }
-            const int nb = ng - g0 + 1 < GB ? ng - g0 + 1 : GB;  // wave-uniform
-#pragma unroll 4
-            for (int st = 0; st < (int)seg; ++st)
-#pragma unroll
-                for (int q = 0; q < GB; ++q)
-                    if (q < nb) slide_step<JB, NF, DETREND>(acc[q], om, u + ((g0 + q - 1) * (int)seg + st) * REC, sb[q]);
-#pragma unroll
-            for (int q = 0; q < GB; ++q) {
-                if (q >= nb) break;
-#pragma unroll
-                for (int i = 0; i < JB; ++i)
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) trk[i][f] = cmul(ps[i][f], trk[i][f]) + acc[q][i][f];
-                sum += sb[q];
-                put(g0 + q);
-            }
-        }
-        if (trc) trc[4] = trc[5] = wall_clock64();
-        return;
-    }
     for (int g = 1; g < chain; ++g) {
         const int64_t wsg0 = g * seg;  // this segment's first window, relative to w0
         if (wsg0 > nsteps) break;

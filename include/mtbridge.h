@@ -319,9 +319,12 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo);
 MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
 /* Tuning (hop = 1 top-k records, N >= 1024): segments per seed workgroup.  The
  * first segment of a chain is seeded by the FFTs, each next one by sliding the
- * band's trackers on from the previous (the scan's own operations, so the
- * records are identical); 1 = one FFT seed per segment, 0 = the library's
- * policy.  Capped at 1 + 256 / segment (a chain's steps are staged in LDS).
+ * band's trackers on from the previous (the scan's own slide operations: the
+ * records agree with FFT seeds within the parity bars); 1 = one FFT seed per
+ * segment, 0 = the library's policy (chains of ~128 windows when the batch is
+ * too small for 64-window segments to fill the GPU -- a strong-scaled shard --
+ * and its segments drop to 32 windows, else 1).  Capped at 1 + 256 / segment
+ * (a chain's steps are staged in LDS).
  * MTB_BAD_ARGS for an unknown plan or segments outside 0..16. */
 MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
 /* Diagnostic: a timeline of the hop = 1 top-k kernels of later executes into
@@ -338,8 +341,10 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch; 0 = the
  *    probe-threshold scan (16 windows per batch, 4 waves per SIMD), 4 / 5 = the
  *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave); 6 =
- *    the default scan with seed chains (one FFT seed per <= 256 windows, the
- *    next segments' seeds by sliding the band on; slower, round 5);
+ *    the default scan with seed chains of <= 256 windows at any segment
+ *    length (one FFT seed per chain, the next segments' seeds by sliding the
+ *    band on; slower on whole batches, round 5); 7 = plain (not non-temporal)
+ *    stores of the seed records;
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams (a one-window
  *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused

@@ -44,6 +44,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--extra", default="", help="extra bench.py arguments, comma-separated")
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="passes over the ranks (and the whole batch); each rank's time = the median of its passes")
     a = ap.parse_args()
     gs = [int(g) for g in re.split("[,+]", a.gpus)]
     extra = [x for x in a.extra.split(",") if x]
@@ -51,28 +53,36 @@ def main() -> int:
     res = {"caveat": "single-GPU emulation, not a scaling curve: each rank's strong-scaling shard is timed alone on "
                      "one MI355X (bench.py --emulate-shard R/G); predicted speed-up = T(whole batch on 1 GPU) / "
                      "max over ranks of T(shard)",
-           "steps": a.steps, "warmup": a.warmup, "configs": {}}
+           "steps": a.steps, "warmup": a.warmup, "repeat": a.repeat, "configs": {}}
     for cfg in re.split("[,+]", a.configs):
         modes = re.split("[,+]", a.c5_shards) if cfg == "c5" else ["windows"]
-        one = run_bench(["--config", cfg] + common, 300)
+        ones = [run_bench(["--config", cfg] + common, 300) for _ in range(a.repeat)]
+        one = sorted(ones, key=lambda x: x["ms_per_step"])[len(ones) // 2]
         t1 = one["ms_per_step"]
         print(f"{cfg} G=1: {t1:.4f} ms ({one['value']:.4g} windows/s, frac {one['roofline']['frac']:.3f})", flush=True)
         for mode in modes:
             key = cfg if cfg != "c5" else f"c5[{mode}]"
-            entry = {"t1_ms": t1, "t1_frac": one["roofline"]["frac"], "split": mode, "by_g": {}}
+            entry = {"t1_ms": t1, "t1_frac": one["roofline"]["frac"], "t1_passes": [x["ms_per_step"] for x in ones],
+                     "split": mode, "by_g": {}}
             for g in gs:
+                runs = {r: [] for r in range(g)}
+                for _ in range(a.repeat):  # passes over the ranks: box drift touches every rank alike
+                    for r in range(g):
+                        args = ["--config", cfg, "--emulate-shard", f"{r}/{g}"] + common
+                        if cfg == "c5":
+                            args += ["--c5-shard", mode]
+                        ln = run_bench(args, 300)
+                        runs[r].append(ln)
+                        print(f"  {key} {r}/{g}: {ln['ms_per_step']:.4f} ms, {ln['config']['windows_per_gpu']} windows, "
+                              f"frac {ln['roofline']['frac']:.3f}", flush=True)
                 ranks = []
                 for r in range(g):
-                    args = ["--config", cfg, "--emulate-shard", f"{r}/{g}"] + common
-                    if cfg == "c5":
-                        args += ["--c5-shard", mode]
-                    ln = run_bench(args, 300)
+                    ln = sorted(runs[r], key=lambda x: x["ms_per_step"])[len(runs[r]) // 2]
                     ranks.append({"rank": r, "ms": ln["ms_per_step"], "kernel_ms": ln["roofline"]["kernel_ms"],
+                                  "ms_passes": [x["ms_per_step"] for x in runs[r]],
                                   "windows": ln["config"]["windows_per_gpu"],
                                   "alg_bytes": ln["roofline"]["algorithmic_bytes_per_launch"],
                                   "frac": ln["roofline"]["frac"], "workload": ln["config"]["workload"]})
-                    print(f"  {key} {r}/{g}: {ln['ms_per_step']:.4f} ms, {ln['config']['windows_per_gpu']} windows, "
-                          f"frac {ln['roofline']['frac']:.3f}", flush=True)
                 worst = max(x["ms"] for x in ranks)
                 mean = sum(x["ms"] for x in ranks) / g
                 entry["by_g"][str(g)] = {"ranks": ranks, "worst_ms": worst, "mean_ms": mean,
