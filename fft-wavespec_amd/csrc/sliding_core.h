@@ -381,11 +381,20 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     // seed records: non-temporal stores (default) -- every workgroup writes its chain's records at its end, and the
     // dirty lines a plain store leaves in L2 are written back at the kernel boundary before the scan can start;
     // variant 7 keeps plain stores
-    const bool nts = a.variant != 7;
+    // variant 8: agent-scope (write-through) stores, so that no dirty seed lines are left in the XCDs' L2s for the
+    // kernel-end writeback
+    const bool nts = a.variant != 7, wt = a.variant == 8;
     auto wst = [&](d2 *p, d2 v) {
         typedef double v2d __attribute__((ext_vector_type(2)));
-        if (nts) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d *>(p));
-        else *p = v;
+        if (wt) {
+            double *q = reinterpret_cast<double *>(p);
+            __hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (nts) {
+            __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d *>(p));
+        } else {
+            *p = v;
+        }
     };
     d2 trk[JB][NF];  // the chain's trackers of bins kmin + t + TP i
     double sum = 0.0;

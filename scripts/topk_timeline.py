@@ -1,7 +1,7 @@
 """Timeline of the hop = 1 top-k pair (seed kernel, then probe scan; wsp_plan_set_trace) on C4 top-8 or one of
 its strong-scaled shards: where the time goes -- FFT seeds, seed chains, scan workgroups, gaps.
 
-    python scripts/topk_timeline.py <out.json> [R/G[:seg[:chain]] ...]
+    python scripts/topk_timeline.py <out.json> [R/G[:seg[:chain[:variant]]] ...]
 
 For each case (default: 0/8 at the policy's segment, and 0/8:32:4) it builds exactly the workload bench.py times
 (bench.SingleBatch on c4_topk, strong shard), runs 30 warm executes, then one traced execute, and writes a
@@ -24,8 +24,8 @@ def pct(a):
     return [round(float(x), 2) for x in np.percentile(a, [0, 10, 50, 90, 100])] if len(a) else []
 
 
-def run(r, g, seg, chain):
-    wl = bench.SingleBatch("c4_topk", r, 0, g, "strong" if g > 1 else "weak", "auto", seg, 0, 0, chain)
+def run(r, g, seg, chain, variant=0):
+    wl = bench.SingleBatch("c4_topk", r, 0, g, "strong" if g > 1 else "weak", "auto", seg, variant, 0, chain)
     for _ in range(30):
         wl.step()
     torch.cuda.synchronize()
@@ -46,7 +46,7 @@ def run(r, g, seg, chain):
     t0 = seeds[:, 1].min()
     su = (seeds[:, 1:] - t0) / 100.0  # 100 MHz wall clock -> us
     cu = (scans - t0) / 100.0
-    summ = {"case": f"{r}/{g}:{seg or 'auto'}:{chain or 'auto'}", "event_ms": ev[0].elapsed_time(ev[1]),
+    summ = {"case": f"{r}/{g}:{seg or 'auto'}:{chain or 'auto'}:v{variant}", "event_ms": ev[0].elapsed_time(ev[1]),
             "seed_workgroups": int(len(seeds)), "scan_workgroups": int(len(scans)),
             "seed_start": pct(su[:, 0]), "seed_fft0_us": pct(su[:, 1] - su[:, 0]), "seed_fft1_us": pct(su[:, 2] - su[:, 1]),
             "seed_chain_us": pct(su[:, 3] - su[:, 2]), "seed_end": pct(su[:, 4]),
@@ -64,7 +64,8 @@ def main():
         r, g = (int(v) for v in rg.split("/"))
         seg = int(rest[0]) if rest else 0
         chain = int(rest[1]) if len(rest) > 1 else 0
-        cases.append((r, g, seg, chain))
+        variant = int(rest[2]) if len(rest) > 2 else 0
+        cases.append((r, g, seg, chain, variant))
     from wavespec_amd import bridge
     bridge.init(0, 16)
     res = [run(*c) for c in cases]
