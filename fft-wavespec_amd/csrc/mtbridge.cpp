@@ -2041,9 +2041,9 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 9;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..8", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..9", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);

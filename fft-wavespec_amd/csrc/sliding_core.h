@@ -378,12 +378,12 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void slide_seed_r_kernel(SlideAr
     const int64_t stride = slide_topk_seed_stride(NF, a.span);
     d2 *__restrict__ ws = static_cast<d2 *>(a.ws) + sg0 * stride;
     const int span = a.span, kmin = a.kmin;
-    // seed records: non-temporal stores (default) -- every workgroup writes its chain's records at its end, and the
-    // dirty lines a plain store leaves in L2 are written back at the kernel boundary before the scan can start;
-    // variant 7 keeps plain stores
-    // variant 8: agent-scope (write-through) stores, so that no dirty seed lines are left in the XCDs' L2s for the
-    // kernel-end writeback
-    const bool nts = a.variant != 7, wt = a.variant == 8;
+    // seed records: agent-scope (write-through, sc1) stores -- every workgroup of a chain writes its later segments'
+    // records at its end, and the dirty lines plain or non-temporal stores leave in the XCDs' L2s are written back at
+    // the kernel boundary before the scan can start: 1/8 C4 top-8 0.0781 / 0.0784 ms (non-temporal), 0.0774 / 0.0785
+    // (plain, variant 7), 0.0732 / 0.0733 (write-through), first scan workgroup 31.0 / 30.3 / 25.1 us after the first
+    // seed workgroup's start (r05r, profiles/r05/timeline); the whole batch unchanged.  Variant 8 = non-temporal.
+    const bool nts = a.variant == 8, wt = a.variant != 7 && a.variant != 8;
     auto wst = [&](d2 *p, d2 v) {
         typedef double v2d __attribute__((ext_vector_type(2)));
         if (wt) {
@@ -928,7 +928,13 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
                         const int ci = real ? mw * C + tb[s] : 0;
                         const d2 v = cx[ci];
                         const int bj = cb[ci];
-                        *reinterpret_cast<d4 *>(o + 4 * s) = real ? d4{(double)(kmin + bj), tp[s], v.x, v.y} : d4{-1.0, -1.0, 0.0, 0.0};
+                        const d4 rv = real ? d4{(double)(kmin + bj), tp[s], v.x, v.y} : d4{-1.0, -1.0, 0.0, 0.0};
+                        if (a.variant == 9) {  // ablation: write-through record stores
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) __hip_atomic_store(o + 4 * s + e, rv[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else {
+                            *reinterpret_cast<d4 *>(o + 4 * s) = rv;
+                        }
                         if (real) atomicOr(&nm[bj], 1u << mw);
                     }
                 }

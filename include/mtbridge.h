@@ -334,7 +334,7 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  * 2 b, each while it fits.  capacity = 0 turns it off (the default).
  * MTB_BAD_ARGS for an unknown plan or a null buffer. */
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
-/* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..9 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -343,8 +343,9 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    same at 32 windows x 16 candidates / 32 x 12 (more LDS per wave); 6 =
  *    the default scan with seed chains of <= 256 windows at any segment
  *    length (one FFT seed per chain, the next segments' seeds by sliding the
- *    band on; slower on whole batches, round 5); 7 = plain (not non-temporal)
- *    stores of the seed records, 8 = agent-scope (write-through) ones;
+ *    band on; slower on whole batches, round 5); 7 = plain stores of the seed
+ *    records, 8 = non-temporal ones (the default writes them through to
+ *    memory, agent scope); 9 = write-through stores of the records too;
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams (a one-window
  *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused
