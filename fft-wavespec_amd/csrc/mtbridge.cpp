@@ -1294,6 +1294,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     SlideMix m{};
     m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
     m.seed_lds = g.mode == 5;        // ablation: the round-4 seed FFTs
+    m.wt = g.mode == 6;              // output rows written through to memory (sc1)
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;
@@ -1315,7 +1316,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     if (policy) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
         above_floor = S > 128;
-        small = !above_floor && g.mode == 0;
+        small = !above_floor && (g.mode == 0 || g.mode == 6);
         S = std::min<int64_t>(256, std::max<int64_t>(128, S));
     }
     // Half-length segments for the last class (the shortest windows, picked up last, drain the launch) when the
@@ -1324,7 +1325,7 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     // floor, where halving only adds seeds) ran 5 % slower with them.  Mode 3: at every size; mode 4: never (A/B).
     const int last_l2 = g.cfg[order[n - 1]].log2n;
     const bool tail_half = policy && g.cfg[order[0]].log2n != last_l2 &&
-                           (g.mode == 3 || ((g.mode == 0 || g.mode == 2 || g.mode == 5) && above_floor));
+                           (g.mode == 3 || ((g.mode == 0 || g.mode == 2 || g.mode == 5 || g.mode == 6) && above_floor));
     Tables t4096;
     int st = get_tables(g.dev, 12, false, &t4096);
     if (st != MTB_OK) return st;
@@ -2041,9 +2042,9 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 9;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..9", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..8", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);
@@ -2308,8 +2309,8 @@ MTB_API int32_t wsp_group_launches(int64_t group) {
 
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode) {
     std::shared_ptr<Group> g = find_group(group);
-    if (!g || mode < 0 || mode > 5) {
-        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..5", (long long)group, mode);
+    if (!g || mode < 0 || mode > 6) {
+        set_error("wsp_group_set_mode(%lld, %d): unknown group or mode outside 0..6", (long long)group, mode);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(g->mu);

@@ -265,6 +265,12 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     SlideArgs ua{};
     ua.s0 = m->s0, ua.s1 = m->s1, ua.s2 = m->s2, ua.c1 = c1, ua.sn1 = sn1, ua.c2 = c2, ua.sn2 = sn2;
     T *__restrict__ out = static_cast<T *>(outp) + w0 * M + 2 * t;
+    // write-through form (m->wt): buffer stores with the sc1 policy at byte offsets from the member's output (< 2 GiB
+    // per member: 20000 windows x 2048 bins x 8 B), so no dirty output lines wait in the XCDs' L2s for the writeback
+    // at the end of the launch
+    const bool wt = m->wt != 0;
+    const __amdgpu_buffer_rsrc_t orc = __builtin_amdgcn_make_buffer_rsrc(outp, (short)0, 0x7fffffff, 0x00020000);
+    uint32_t ob = (uint32_t)((w0 * M + 2 * t) * (int64_t)sizeof(T));
     double *u = reinterpret_cast<double *>(buf);
     for (int c0 = 0; c0 < maxlen; c0 += CH) {
         const int clen = maxlen - c0 < CH ? maxlen - c0 : CH;
@@ -288,9 +294,22 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
 #pragma unroll
             for (int q = 0; q < B / 2; ++q) {
                 typedef T v2t __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
+                const v2t pv = v2t{(T)pw[2 * q], (T)pw[2 * q + 1]};
+                if (wt) {
+                    const int qo = (int)(ob + 2 * NT * q * sizeof(T));
+                    if constexpr (sizeof(T) == 8) {
+                        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, pv), orc, qo, 0, 16);
+                    } else {
+                        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, pv), orc, qo, 0, 16);
+                    }
+                } else {
+                    *reinterpret_cast<v2t *>(out + 2 * NT * q) = pv;
+                }
             }
             out += M;
+            ob += M * sizeof(T);
             if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
         }
     }

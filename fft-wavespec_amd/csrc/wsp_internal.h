@@ -169,6 +169,7 @@ struct SlideMix {
     int nclass, n_tasks;
     int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
     int seed_lds;                       // 1: the round-4 seed FFTs (staged inputs, radix-4 LDS passes; ablation)
+    int wt;                             // 1: output rows written through to memory (sc1 buffer stores), else plain
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];

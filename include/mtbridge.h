@@ -334,7 +334,7 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  * 2 b, each while it fits.  capacity = 0 turns it off (the default).
  * MTB_BAD_ARGS for an unknown plan or a null buffer. */
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
-/* Tuning / ablation: the kernel form, 0..9 (MTB_BAD_ARGS outside); 0 = the
+/* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
@@ -345,7 +345,7 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    length (one FFT seed per chain, the next segments' seeds by sliding the
  *    band on; slower on whole batches, round 5); 7 = plain stores of the seed
  *    records, 8 = non-temporal ones (the default writes them through to
- *    memory, agent scope); 9 = write-through stores of the records too;
+ *    memory, agent scope);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams (a one-window
  *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused
@@ -445,8 +445,10 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * for the shortest window length, which drains the launch, at every batch
  * size (the default does so only when the batch is large enough that the
  * segment policy is above its floor of 128 windows); 4 = the mixed launch
- * with one segment length for every window length (ablation).  MTB_BAD_ARGS
- * outside 0..4. */
+ * with one segment length for every window length (ablation); 5 = the mixed
+ * launch with the round-4 seed FFTs through LDS (ablation); 6 = the mixed
+ * launch with its output rows written through to memory (agent-scope sc1
+ * stores).  MTB_BAD_ARGS outside 0..6. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 /* Diagnostic: a per-task timeline of the mixed-length launch.  d_trace = a
  * device buffer of 4 x capacity_tasks int64: task t of each later execute

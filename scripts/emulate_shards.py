@@ -43,12 +43,12 @@ def main() -> int:
     ap.add_argument("--c5-shards", default="split,split-time,symbols")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--extra", default="", help="extra bench.py arguments, comma-separated")
+    ap.add_argument("--extra", default="", help="extra bench.py arguments, comma- or plus-separated")
     ap.add_argument("--repeat", type=int, default=1,
                     help="passes over the ranks (and the whole batch); each rank's time = the median of its passes")
     a = ap.parse_args()
     gs = [int(g) for g in re.split("[,+]", a.gpus)]
-    extra = [x for x in a.extra.split(",") if x]
+    extra = [x for x in re.split("[,+]", a.extra) if x]
     common = ["--steps", str(a.steps), "--warmup", str(a.warmup)] + extra
     res = {"caveat": "single-GPU emulation, not a scaling curve: each rank's strong-scaling shard is timed alone on "
                      "one MI355X (bench.py --emulate-shard R/G); predicted speed-up = T(whole batch on 1 GPU) / "

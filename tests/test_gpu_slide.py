@@ -524,7 +524,8 @@ def test_stateful_plan_on_two_streams(gpu_session, kind):
     plan.close()
 
 
-@pytest.mark.parametrize("mode", ["auto", "per-length", "mixed-b4", "mixed-tail-half", "mixed-uniform", "mixed-lds-seeds"])
+@pytest.mark.parametrize("mode", ["auto", "per-length", "mixed-b4", "mixed-tail-half", "mixed-uniform", "mixed-lds-seeds",
+                                  "mixed-write-through"])
 @pytest.mark.parametrize("prec,detrend,window", [("f64", "none", "hann"), ("f64", "mean", "blackman"),
                                                  ("f32", "mean", "hamming"), ("f64", "none", "none")])
 def test_group_mixed_members(gpu_session, prec, detrend, window, mode):
