@@ -75,7 +75,7 @@ def parse(argv=None):
                          "default, one per window length up to 4) / streams the symbol plans use (0 = 3)")
     ap.add_argument("--c5-mode", default="group",
                     choices=["group", "group-per-length", "group-mixed-b4", "group-mixed-tail-half", "group-mixed-uniform",
-                             "group-mixed-lds-seeds", "group-mixed-write-through", "plans"],
+                             "group-mixed-lds-seeds", "group-mixed-plain-stores", "plans"],
                     help="C5: one grouped device plan (wsp_group_*: one mixed-length persistent launch), the grouped "
                          "plan's per-length launches on lanes (round-3 form), the mixed launch with four bins per thread "
                          "for N <= 1024 / half-length segments for the shortest window length at every size / one segment length (wsp_group_set_mode 2 / 3 / 4, "
@@ -462,14 +462,14 @@ class C5Batch(Workload):
             if c5_mode == "group-per-length":
                 self.group.set_mode("per-length")
             elif c5_mode in ("group-mixed-b4", "group-mixed-tail-half", "group-mixed-uniform", "group-mixed-lds-seeds",
-                             "group-mixed-write-through"):
+                             "group-mixed-plain-stores"):
                 self.group.set_mode(c5_mode[len("group-"):])
             if c5_streams:
                 self.group.set_streams(c5_streams)
             if slide_seg:
                 self.group.set_segment(slide_seg)
             self._ptrs = ([x.data_ptr() for x in self.series], [o.data_ptr() for o in self.outs])
-            self.algorithm = "slide-group" + {"group-per-length": "-per-length", "group-mixed-b4": "-mixed-b4", "group-mixed-tail-half": "-mixed-tail-half", "group-mixed-uniform": "-mixed-uniform", "group-mixed-lds-seeds": "-mixed-lds-seeds", "group-mixed-write-through": "-mixed-write-through"}.get(c5_mode, "")
+            self.algorithm = "slide-group" + {"group-per-length": "-per-length", "group-mixed-b4": "-mixed-b4", "group-mixed-tail-half": "-mixed-tail-half", "group-mixed-uniform": "-mixed-uniform", "group-mixed-lds-seeds": "-mixed-lds-seeds", "group-mixed-plain-stores": "-mixed-plain-stores"}.get(c5_mode, "")
             self.layout = {"mode": "group", "launches": self.group.launches, "streams": c5_streams or "library default",
                            "segment": slide_seg or "auto", "pieces": len(pieces)}
             self.windows = sum(p[2] for p in pieces)

@@ -522,6 +522,7 @@ int slide_args(int dev, const Config &c, SlideArgs *A) {
     A->s0 = wc.a0, A->s1 = wc.a1 / 2, A->s2 = wc.a2 / 2;
     A->c1 = (double)cosl(th), A->sn1 = (double)sinl(th), A->c2 = (double)cosl(2 * th), A->sn2 = (double)sinl(2 * th);
     A->inv_n = 1.0 / c.n;
+    A->store_wt = c.variant == 7;  // hop = 1 power rows written through (A/B, round 5)
     return MTB_OK;
 }
 
@@ -1294,7 +1295,9 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     SlideMix m{};
     m.bsmall = g.mode == 2 ? 4 : 2;  // measured: 0.737 ms (2) against 0.777 (4) for C5, profiles/r04/ab
     m.seed_lds = g.mode == 5;        // ablation: the round-4 seed FFTs
-    m.wt = g.mode == 6;              // output rows written through to memory (sc1)
+    // output rows written through to memory (sc1 stores; mode 6 = plain): no dirty output lines wait in the XCDs' L2s
+    // for the writeback at the end of the launch -- C5 0.7275 / 0.7298 -> 0.7024 / 0.7114 ms (r05t, one box)
+    m.wt = g.mode != 6;
     const Config &c0 = g.cfg[order[0]];
     const int nf = window_coef(c0.window).nf;
     const int det = c0.detrend == MTB_DETREND_MEAN ? kDetrendMean : kDetrendNone;

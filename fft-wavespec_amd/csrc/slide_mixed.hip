@@ -265,12 +265,13 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
     SlideArgs ua{};
     ua.s0 = m->s0, ua.s1 = m->s1, ua.s2 = m->s2, ua.c1 = c1, ua.sn1 = sn1, ua.c2 = c2, ua.sn2 = sn2;
     T *__restrict__ out = static_cast<T *>(outp) + w0 * M + 2 * t;
-    // write-through form (m->wt): buffer stores with the sc1 policy at byte offsets from the member's output (< 2 GiB
-    // per member: 20000 windows x 2048 bins x 8 B), so no dirty output lines wait in the XCDs' L2s for the writeback
-    // at the end of the launch
+    // write-through form (m->wt, the default): buffer stores with the sc1 policy, so no dirty output lines wait in the
+    // XCDs' L2s for the writeback at the end of the launch; the descriptor is based at the segment's first row (uniform
+    // per sub-workgroup), the offsets stay within the segment (<= 2048 rows x 2048 bins x 8 B)
     const bool wt = m->wt != 0;
-    const __amdgpu_buffer_rsrc_t orc = __builtin_amdgcn_make_buffer_rsrc(outp, (short)0, 0x7fffffff, 0x00020000);
-    uint32_t ob = (uint32_t)((w0 * M + 2 * t) * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t orc =
+        __builtin_amdgcn_make_buffer_rsrc(static_cast<T *>(outp) + w0 * M, (short)0, 0x7fffffff, 0x00020000);
+    uint32_t ob = (uint32_t)(2 * t * (int)sizeof(T));
     double *u = reinterpret_cast<double *>(buf);
     for (int c0 = 0; c0 < maxlen; c0 += CH) {
         const int clen = maxlen - c0 < CH ? maxlen - c0 : CH;

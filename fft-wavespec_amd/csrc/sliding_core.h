@@ -267,6 +267,12 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
     }
 
     T *__restrict__ out = static_cast<T *>(sg.out) + sg.w0 * M + 2 * t;
+    // a.store_wt: sc1 buffer stores (written through to memory: no dirty rows left in the XCDs' L2s for the writeback
+    // at the kernel's end), the descriptor at the segment's first row, offsets within the segment
+    const bool wt = a.store_wt != 0;
+    const __amdgpu_buffer_rsrc_t orc =
+        __builtin_amdgcn_make_buffer_rsrc(static_cast<T *>(sg.out) + sg.w0 * M, (short)0, 0x7fffffff, 0x00020000);
+    uint32_t ob = (uint32_t)(2 * t * (int)sizeof(T));
     double *u = reinterpret_cast<double *>(lds);
     for (int c0 = 0; c0 < len; c0 += CH) {
         const int clen = len - c0 < CH ? len - c0 : CH;
@@ -294,9 +300,22 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
 #pragma unroll
             for (int q = 0; q < B / 2; ++q) {
                 typedef T v2t __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<v2t *>(out + 2 * NT * q) = v2t{(T)p[2 * q], (T)p[2 * q + 1]};
+                const v2t pv = v2t{(T)p[2 * q], (T)p[2 * q + 1]};
+                if (wt) {
+                    const int qo = (int)(ob + 2 * NT * q * sizeof(T));
+                    if constexpr (sizeof(T) == 8) {
+                        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, pv), orc, qo, 0, 16);
+                    } else {
+                        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, pv), orc, qo, 0, 16);
+                    }
+                } else {
+                    *reinterpret_cast<v2t *>(out + 2 * NT * q) = pv;
+                }
             }
             out += M;
+            ob += M * sizeof(T);
             if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
         }
     }

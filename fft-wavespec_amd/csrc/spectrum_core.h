@@ -204,6 +204,7 @@ enum Var : int {
     kVarLdsB64 = 4096,  // with kVarSplitLds: exchange reads as single ds_read_b64 (no ds_read2_b64 pairing)
     kVarWinTab = 8192,  // window values (with the R2C factor 1/2) from an fp64 table a.win (L1/L2-resident)
     kVarVec = 16384,    // sample pairs known 2-element aligned: one 16-B (8-B) load per pair, no run-time test of a.vec
+    kVarWtStore = 32768,  // power rows written through to memory (agent-scope sc1 buffer stores), no dirty L2 lines
 };
 
 // Workgroup shape of a variant: kVarWave1 shrinks the workgroup to one wave
@@ -1635,8 +1636,17 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                 for (int j = 0; j < 16 / VE; ++j) {
                     const int k = VE * (t + TPW * j);
                     const vst val = *reinterpret_cast<const vst *>(prow + k);
-                    if constexpr (VAR & kVarNtStore) __builtin_nontemporal_store(val, reinterpret_cast<vst *>(a.out + w * M + k));
-                    else *reinterpret_cast<vst *>(a.out + w * M + k) = val;
+                    if constexpr (VAR & kVarWtStore) {  // descriptor at the group's first row: uniform, small offsets
+                        const __amdgpu_buffer_rsrc_t orc =
+                            __builtin_amdgcn_make_buffer_rsrc(a.out + g * WPB * (int64_t)M, (short)0, 0x7fffffff, 0x00020000);
+                        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, val), orc,
+                                                               (int)((slot * M + k) * (int)sizeof(T)), 0, 16);
+                    } else if constexpr (VAR & kVarNtStore) {
+                        __builtin_nontemporal_store(val, reinterpret_cast<vst *>(a.out + w * M + k));
+                    } else {
+                        *reinterpret_cast<vst *>(a.out + w * M + k) = val;
+                    }
                 }
             }
         }

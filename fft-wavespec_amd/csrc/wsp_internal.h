@@ -137,6 +137,7 @@ struct SlideArgs {
                           // segments fill 1/share of the resident workgroup slots; 0 / 1 = all of them
     int seed_chain;       // top-k seeds (N >= 1024): segments per seed workgroup -- one FFT seed, the next ones by
                           // sliding the band's trackers seg windows at a time (<= 1: one FFT seed per segment)
+    int store_wt;         // slide_kernel power rows: 1 = written through to memory (sc1 buffer stores), 0 = plain
     long long *trace;     // diagnostic (wsp_plan_set_trace): top-k seed workgroup b writes 6 ticks at 6 b, scan workgroup
     int64_t trace_cap;    // b 2 ticks at trace_cap / 2 + 2 b, while they fit in trace_cap int64 entries; nullptr = off
 };
@@ -169,7 +170,7 @@ struct SlideMix {
     int nclass, n_tasks;
     int bsmall;                         // bins per thread for N <= 1024: 2 (default) or 4; N >= 2048 always 4
     int seed_lds;                       // 1: the round-4 seed FFTs (staged inputs, radix-4 LDS passes; ablation)
-    int wt;                             // 1: output rows written through to memory (sc1 buffer stores), else plain
+    int wt;                             // 1: output rows written through to memory (sc1 buffer stores; default), 0: plain
     int log2n[kMixClass], seg[kMixClass];
     int task0[kMixClass], nseg[kMixClass], mem0[kMixClass + 1];  // first task / segments / first member of class c
     double c1[kMixClass], sn1[kMixClass], c2[kMixClass], sn2[kMixClass], inv_n[kMixClass];

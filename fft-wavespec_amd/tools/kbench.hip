@@ -340,8 +340,11 @@ int main(int argc, char **argv) {
             const float d = time_variant<kDefaultVar>(L, s, reps);
             L.nt_mode = 1;
             const float e = time_variant<kDefaultVar | kVarNtLoad | kVarVec>(L, s, reps);
-            printf("round %d  nt-store %7.1f us %6.0f GB/s | plain-store %7.1f us %6.0f GB/s | plain-store, cached loads %7.1f us %6.0f GB/s | run-time nt loads %7.1f us %6.0f GB/s | nt + compile-time pair loads %7.1f us %6.0f GB/s\n",
-                   round, a, bytes / a / 1e3, b, bytes / b / 1e3, c, bytes / c / 1e3, d, bytes / d / 1e3, e, bytes / e / 1e3);
+            const float f = time_variant<kDefaultVar | kVarNtLoad | kVarWtStore>(L, s, reps);
+            const float g = time_variant<kDefaultVar | kVarNtLoad | kVarVec | kVarWtStore>(L, s, reps);
+            printf("round %d  nt-store %7.1f us %6.0f GB/s | plain-store %7.1f us %6.0f GB/s | plain-store, cached loads %7.1f us %6.0f GB/s | run-time nt loads %7.1f us %6.0f GB/s | nt + compile-time pair loads %7.1f us %6.0f GB/s | write-through store %7.1f us %6.0f GB/s | wt + pair loads %7.1f us %6.0f GB/s\n",
+                   round, a, bytes / a / 1e3, b, bytes / b / 1e3, c, bytes / c / 1e3, d, bytes / d / 1e3, e, bytes / e / 1e3,
+                   f, bytes / f / 1e3, g, bytes / g / 1e3);
             fflush(stdout);
         }
         return 0;

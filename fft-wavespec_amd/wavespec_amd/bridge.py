@@ -409,7 +409,7 @@ class Group:
         _check("wsp_group_set_segment", lib().wsp_group_set_segment(self.handle, windows))
 
     MODES = {"auto": 0, "per-length": 1, "mixed-b4": 2, "mixed-tail-half": 3, "mixed-uniform": 4, "mixed-lds-seeds": 5,
-             "mixed-write-through": 6}
+             "mixed-plain-stores": 6}
 
     def set_mode(self, mode: str) -> None:
         """"auto": one mixed-length persistent launch where eligible; "per-length": one launch per window length;

@@ -447,8 +447,8 @@ MTB_API int32_t wsp_group_set_segment(int64_t group, int64_t windows);
  * segment policy is above its floor of 128 windows); 4 = the mixed launch
  * with one segment length for every window length (ablation); 5 = the mixed
  * launch with the round-4 seed FFTs through LDS (ablation); 6 = the mixed
- * launch with its output rows written through to memory (agent-scope sc1
- * stores).  MTB_BAD_ARGS outside 0..6. */
+ * launch with plain output stores (the mixed launch writes its output rows
+ * through to memory: agent-scope sc1 stores).  MTB_BAD_ARGS outside 0..6. */
 MTB_API int32_t wsp_group_set_mode(int64_t group, int32_t mode);
 /* Diagnostic: a per-task timeline of the mixed-length launch.  d_trace = a
  * device buffer of 4 x capacity_tasks int64: task t of each later execute

@@ -72,6 +72,27 @@ def test_slide_f32(gpu_session, n):
     plan.close()
 
 
+@pytest.mark.parametrize("n,prec,seg", [(512, "f64", 0), (2048, "f64", 0), (4096, "f32", 0), (8192, "f64", 0),
+                                        (1024, "f64", 2048), (2048, "f32", 37)])
+def test_slide_write_through_rows(gpu_session, n, prec, seg):
+    """The power rows written through to memory (sc1 buffer stores at offsets from each segment's first row,
+    wsp_plan_set_variant 7) are the plain stores' rows bit for bit: ragged batches, the longest segment, odd ones."""
+    torch = pytest.importorskip("torch")
+    nwin = 3000 + n // 16
+    s = synth.random_walk(nwin + n - 1, seed=n + 11)
+    dt = torch.float64 if prec == "f64" else torch.float32
+    outs = []
+    for v in (0, 7):
+        plan = bridge.Plan(0, n, 1, nwin, "none", "hann", 0, prec)
+        plan.set_algorithm("slide")
+        plan.set_variant(v)
+        if seg:
+            plan.set_slide_segment(seg)
+        outs.append(_run(plan, s, torch, dt))
+        plan.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("nwin", [1, 2, 63, 64, 65, 511, 512, 513, 4097])
 def test_slide_segment_seams(gpu_session, nwin):
     """Batch sizes around the segment and staging-chunk lengths and a single window."""
@@ -525,7 +546,7 @@ def test_stateful_plan_on_two_streams(gpu_session, kind):
 
 
 @pytest.mark.parametrize("mode", ["auto", "per-length", "mixed-b4", "mixed-tail-half", "mixed-uniform", "mixed-lds-seeds",
-                                  "mixed-write-through"])
+                                  "mixed-plain-stores"])
 @pytest.mark.parametrize("prec,detrend,window", [("f64", "none", "hann"), ("f64", "mean", "blackman"),
                                                  ("f32", "mean", "hamming"), ("f64", "none", "none")])
 def test_group_mixed_members(gpu_session, prec, detrend, window, mode):
