@@ -563,7 +563,9 @@ __device__ __forceinline__ bool kagree(float a, float b, float floor_) {
 // then need vmcnt(#stores) instead of vmcnt(0) (gfx950 counts loads and stores in one in-order
 // counter, and the unrotated loop's entry path and conditional stores forced a wait for the previous
 // tile's stores every J steps).
-template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true>
+// SCP: cache policy of the detrended rows' stores (16 = sc1: written through to memory, so none are left dirty in
+// the XCDs' L2s for the writeback between the filter and the spectrum launch; 0 = plain)
+template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true, int SCP = 0>
 __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
                                                                 int64_t hop, int64_t n_windows, int n, KP kp,
                                                                 unsigned *fallbacks = nullptr) {
@@ -591,7 +593,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     };
     auto st4 = [&](f4v v, uint32_t voff, uint32_t soff) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)voff, (int)soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)voff, (int)soff, SCP);
     };
     f4v ra[8], rb[8];
     auto issue = [&](int c) {

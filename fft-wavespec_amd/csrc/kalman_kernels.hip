@@ -45,9 +45,15 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
 // (kalman_bench time, C3: 0.55-0.58 ms against 0.60-0.65 ms for 4-wave workgroups, 0.78-0.81 ms
 // for the four-segment lane-pair kernel at two waves per SIMD, 0.69 ms sequential).
 hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
-    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1>), dim3((unsigned)((L.n_windows + 63) / 64)), dim3(64), 0, stream,
-                       static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp,
-                       (unsigned *)nullptr);
+    // variant 7: the detrended rows written through to memory (A/B, round 5)
+    if (L.variant == 7)
+        hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1, kcore::kPk2Warm, true, 16>), dim3((unsigned)((L.n_windows + 63) / 64)),
+                           dim3(64), 0, stream, static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop,
+                           L.n_windows, L.n, kp, (unsigned *)nullptr);
+    else
+        hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1>), dim3((unsigned)((L.n_windows + 63) / 64)), dim3(64), 0, stream,
+                           static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp,
+                           (unsigned *)nullptr);
     return hipGetLastError();
 }
 
@@ -65,7 +71,7 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
     constexpr int kFixed = kcore::kKfAdapt | kcore::kKfClip;
     const bool fixed = kcore::kalman_flags(kp) == kFixed;
     if (L.f32) {
-        if (fixed && L.variant == 0 && kcore::pk2_fits(L.n)) return launch_pk2(L, kp, stream);
+        if (fixed && (L.variant == 0 || L.variant == 7) && kcore::pk2_fits(L.n)) return launch_pk2(L, kp, stream);
         return fixed ? launch_t<float, kFixed>(L, kp, stream) : launch_t<float, kcore::kKfRuntime>(L, kp, stream);
     }
     return fixed ? launch_t<double, kFixed>(L, kp, stream) : launch_t<double, kcore::kKfRuntime>(L, kp, stream);

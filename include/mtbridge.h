@@ -336,6 +336,10 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
 /* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
+ *  - hop = 1 power rows by the sliding DFT: 7 = plain stores (the default
+ *    writes the rows through to memory, agent-scope sc1 stores);
+ *  - fp32 Kalman pre-pass (two-segment form): 7 = its detrended rows written
+ *    through to memory;
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
  *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch; 0 = the

@@ -75,8 +75,9 @@ def test_slide_f32(gpu_session, n):
 @pytest.mark.parametrize("n,prec,seg", [(512, "f64", 0), (2048, "f64", 0), (4096, "f32", 0), (8192, "f64", 0),
                                         (1024, "f64", 2048), (2048, "f32", 37)])
 def test_slide_write_through_rows(gpu_session, n, prec, seg):
-    """The power rows written through to memory (sc1 buffer stores at offsets from each segment's first row,
-    wsp_plan_set_variant 7) are the plain stores' rows bit for bit: ragged batches, the longest segment, odd ones."""
+    """The power rows written through to memory (sc1 buffer stores at offsets from each segment's first row, the
+    default) are the plain stores' rows (wsp_plan_set_variant 7) bit for bit: ragged batches, the longest segment,
+    odd ones."""
     torch = pytest.importorskip("torch")
     nwin = 3000 + n // 16
     s = synth.random_walk(nwin + n - 1, seed=n + 11)
