@@ -937,55 +937,7 @@ __global__ __launch_bounds__(64, (NB > 2 && LB > 2) ? 2 : LB) void slide_topk_p_
                 topk_insert<K>(tp, tb, on ? v.x * v.x + v.y * v.y : -1.0, on ? i : kEmpty);  // i: ascending bins
             }
             merge_parts<K, WB, LPW>(tp, tb);  // (power desc, index asc): the sequential insertion's order
-            // Records written through to memory as whole lines (default where the candidate list's LDS holds a batch of
-            // records: C >= 2 K): every lane of a window holds the merged list, lane q builds slots q PER .. q PER +
-            // PER - 1, the batch's records are staged in the candidates' LDS and leave as 16 B per lane, 1 KiB per wave
-            // instruction, through sc1 buffer stores -- no dirty record lines in the XCDs' L2s at the kernel's end (the
-            // next execute's seed launch waits for that writeback).  Windows the exact scan wrote (cnt < 0) are skipped.
-            // Variant 7 keeps lane q = 0 storing its window's slots with plain stores.
-            constexpr bool kStage = C * 2 >= 4 * K && K % LPW == 0;
-            if (kStage && a.variant != 7) {
-                constexpr int PER = K / LPW;
-                typedef double d4 __attribute__((ext_vector_type(4)));
-                d4 rv[PER];
-#pragma unroll
-                for (int e = 0; e < PER; ++e) {
-                    const int s = q * PER + e;
-                    double ps = tp[0];
-                    int bs = tb[0];
-#pragma unroll
-                    for (int i = 1; i < K; ++i) {  // slot s of the lists by selects (register arrays: compile-time indices)
-                        ps = s == i ? tp[i] : ps;
-                        bs = s == i ? tb[i] : bs;
-                    }
-                    const bool real = n >= 0 && s < kk && bs != kEmpty;
-                    const int ci = real ? mw * C + bs : 0;
-                    const d2 v = cx[ci];
-                    const int bj = cb[ci];
-                    rv[e] = real ? d4{(double)(kmin + bj), ps, v.x, v.y} : d4{-1.0, -1.0, 0.0, 0.0};
-                    if (real) atomicOr(&nm[bj], 1u << mw);
-                }
-                __syncthreads();  // every candidate read before the records overwrite the candidates' LDS
-                double *stg = reinterpret_cast<double *>(cx);
-                if (n >= 0) {
-#pragma unroll
-                    for (int e = 0; e < PER; ++e) {
-                        const int s = q * PER + e;
-                        if (s < kk) *reinterpret_cast<d4 *>(stg + mw * (4 * kk) + 4 * s) = rv[e];
-                    }
-                }
-                __syncthreads();
-                const int tot = (slot + 1) * (4 * kk);  // doubles of the batch's records, contiguous in the output
-                const __amdgpu_buffer_rsrc_t rrc =
-                    __builtin_amdgcn_make_buffer_rsrc(rec + (int64_t)(wi - slot) * (4 * kk), (short)0, 0x7fffffff, 0x00020000);
-                for (int d = 2 * l; d < tot; d += 128) {
-                    if (cnt[d / (4 * kk)] < 0) continue;  // the exact scan's record
-                    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-                    typedef double d2v __attribute__((ext_vector_type(2)));
-                    const d2v pv = *reinterpret_cast<const d2v *>(stg + d);
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, pv), rrc, d * (int)sizeof(double), 0, 16);
-                }
-            } else if (n >= 0 && q == 0) {
+            if (n >= 0 && q == 0) {
                 double *o = rec + (int64_t)(wi - slot + mw) * (4 * kk);
                 typedef double d4 __attribute__((ext_vector_type(4)));
 #pragma unroll

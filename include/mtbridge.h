@@ -348,9 +348,8 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    the default scan with seed chains of <= 256 windows at any segment
  *    length (one FFT seed per chain, the next segments' seeds by sliding the
  *    band on; slower on whole batches, round 5); 7 = plain stores of the seed
- *    records and of the top-k records, 8 = non-temporal seed-record stores
- *    (the default writes both through to memory, agent scope, the records as
- *    whole lines staged in LDS);
+ *    records, 8 = non-temporal ones (the default writes them through to
+ *    memory, agent scope);
  *  - N = 32768 .. 262144 (four-step transform): 1 = two passes over chunks of
  *    windows; 2 = the same pipelined over two internal streams (a one-window
  *    chunk runs the plain loop: its workspace holds one buffer); 3 = the fused
