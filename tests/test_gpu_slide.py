@@ -498,6 +498,39 @@ def test_slide_topk_refusals(gpu_session):
     p.close()
 
 
+def test_slide_topk_tuning_refusals_and_trace(gpu_session):
+    """wsp_plan_set_seed_chain outside 0..16 and wsp_plan_set_trace with a null buffer are refused and leave the
+    plan usable; a traced execute writes every seed / scan workgroup's ticks in order and the same records."""
+    torch = pytest.importorskip("torch")
+    n, nwin = 2048, 6000
+    s = synth.random_walk(nwin + n - 1, seed=77)
+    p = bridge.Plan(0, n, 1, nwin, "none", "hann", output="topk")
+    p.set_topk(8, 18.0, 200.0)
+    p.set_algorithm("slide")
+    for bad in (-1, 17):
+        with pytest.raises(bridge.BridgeError):
+            p.set_seed_chain(bad)
+    with pytest.raises(bridge.BridgeError):
+        p.set_trace(0, 64)
+    p.set_slide_segment(32)
+    p.set_seed_chain(4)
+    plain = _run(p, s, torch)
+    cap = 6 * 4096
+    tr = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    p.set_trace(tr.data_ptr(), cap)
+    traced = _run(p, s, torch)
+    p.set_trace(0, 0)
+    p.close()
+    assert np.array_equal(plain, traced)
+    t = tr.cpu().numpy()
+    nseg = (nwin + 31) // 32
+    seeds = t[: cap // 2].reshape(-1, 6)[: (nseg + 3) // 4]
+    scans = t[cap // 2:].reshape(-1, 2)[:nseg]
+    assert (seeds[:, 1] > 0).all() and (np.diff(seeds[:, 1:5], axis=1) >= 0).all()
+    assert (scans[:, 0] > 0).all() and (scans[:, 1] >= scans[:, 0]).all()
+    assert scans[:, 0].min() >= seeds[:, 4].max()  # the scan launch starts after every seed workgroup ended
+
+
 def test_slide_topk_host_batch_path(gpu_session):
     """gpu_spectrum_topk_batch (host buffers, chunked per stream, per-part seed workspace) with hop = 1
     takes the sliding top-k per chunk; the per-bar CPU reference is the oracle's scan."""
