@@ -1580,6 +1580,24 @@ MTB_API int32_t gpu_unregister_host(const double *ptr) {
     }
     const HostRegion r = it->second;
     if (r.hi > r.lo) {
+        // Every device of the session idle first: the runtime keeps a registration's GPU mapping (and the driver's
+        // userptr object behind it) alive while commands that used it are not retired, and only retires them at a
+        // synchronisation.  Unregistered but still mapped, the pages are freed by the caller and can come back at the
+        // same address as a later pageable copy's destination, which the runtime then pins over the stale mapping:
+        // the round-5 closing-suite fault (hipErrorIllegalAddress in Tensor.cpu(), reproduced by
+        // test_pageable_copies_after_registrations).  Registrations are long-lived; the wait is rare.
+        int cur = 0;
+        (void)hipGetDevice(&cur);  // the caller's current device is restored below
+        for (auto &d : S->devs) {
+            (void)hipSetDevice(d->dev);
+            if (hipDeviceSynchronize() != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipSetDevice(cur);
+                set_error("gpu_unregister_host: device %d did not synchronise; the buffer is still page-locked", d->dev);
+                return MTB_INTERNAL_ERROR;
+            }
+        }
+        (void)hipSetDevice(cur);
         const hipError_t e = hipHostUnregister((void *)r.lo);
         if (e != hipSuccess) {  // the range stays registered (and in the table): the caller must not free it
             (void)hipGetLastError();
@@ -1587,6 +1605,11 @@ MTB_API int32_t gpu_unregister_host(const double *ptr) {
             return MTB_INTERNAL_ERROR;
         }
         R.regions.erase(it);
+        for (auto &d : S->devs) {  // and the unregistration itself retired before the caller may free the pages
+            (void)hipSetDevice(d->dev);
+            (void)hipDeviceSynchronize();
+        }
+        (void)hipSetDevice(cur);
         if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
             set_error("gpu_unregister_host: HIP still maps [%p, %p) after hipHostUnregister", (void *)r.lo, (void *)r.hi);
             return MTB_INTERNAL_ERROR;
