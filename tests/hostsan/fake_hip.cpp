@@ -31,6 +31,7 @@
 #include <initializer_list>
 #include <map>
 #include <mutex>
+#include <set>
 #include <thread>
 
 #include "../../fft-wavespec_amd/csrc/wsp_internal.h"
@@ -113,6 +114,12 @@ int dev_of(const void *p) {  // -1: not device memory (host, pinned or registere
 // page-locked host ranges: base -> bytes (hipHostRegister)
 std::mutex g_reg_mu;
 std::map<uintptr_t, size_t> g_regs;
+// Streams whose direct copies used a registration since the last device-wide synchronisation: the real runtime
+// kept a registration's mapping alive past hipHostUnregister while the commands that used it were not retired, and
+// the library's own stream synchronisation did not retire them -- a device synchronisation did (the round-5
+// closing-suite fault and its fix) -- so here only hipDeviceSynchronize retires them, and
+// unregistering while any remain counts as a violation.
+std::map<uintptr_t, std::set<ihipStream_t *>> g_reg_users;
 std::atomic<int64_t> g_direct{0};
 bool reg_covers(const void *p, size_t n) {
     const uintptr_t a = (uintptr_t)p;
@@ -222,8 +229,23 @@ hipError_t hipHostUnregister(void *p) {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_regs.find((uintptr_t)p);
     if (it == g_regs.end()) return hipErrorHostMemoryNotRegistered;
+    auto u = g_reg_users.find((uintptr_t)p);
+    if (u != g_reg_users.end() && !u->second.empty()) g_violations++;  // commands that used it not yet retired
+    g_reg_users.erase((uintptr_t)p);
     g_regs.erase(it);
     return hipSuccess;
+}
+void note_reg_use(const void *host, size_t n, ihipStream_t *st) {
+    const uintptr_t a = (uintptr_t)host;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.upper_bound(a);
+    if (it == g_regs.begin()) return;
+    --it;
+    if (a >= it->first && a + n <= it->first + it->second) g_reg_users[it->first].insert(st);
+}
+void retire_reg_uses() {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (auto &u : g_reg_users) u.second.clear();
 }
 // registered / pinned host memory: hipMemoryTypeHost; device memory: hipMemoryTypeDevice; anything else
 // (pageable memory) an error, as the real runtime answers (scripts/hostreg_probe.py)
@@ -260,7 +282,10 @@ hipError_t hipMemset(void *d, int v, size_t n) {
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st) {
     check_op(st, {d, s});
     const void *host = k == hipMemcpyHostToDevice ? s : (k == hipMemcpyDeviceToHost ? d : nullptr);
-    if (host && reg_covers(host, n)) g_direct++;
+    if (host && reg_covers(host, n)) {
+        g_direct++;
+        note_reg_use(host, n, st);
+    }
     run_on(st, [=] { memcpy(d, s, n); });
     return hipSuccess;
 }
@@ -289,8 +314,11 @@ hipError_t hipStreamDestroy(hipStream_t s) {
     return hipSuccess;
 }
 hipError_t hipDeviceSynchronize(void) {
-    std::lock_guard<std::mutex> lk(g_streams_mu);
-    for (auto *s : g_streams) s->drain();
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        for (auto *s : g_streams) s->drain();
+    }
+    retire_reg_uses();
     return hipSuccess;
 }
 hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned int) {
