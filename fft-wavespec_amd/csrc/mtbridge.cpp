@@ -1505,6 +1505,22 @@ MTB_API void gpu_shutdown(void) {
     }
 }
 
+// gpu_set_host_locking: whether gpu_register_host page-locks the caller's memory (1) or only records the range (0,
+// the default: batches on it stage through the library's pinned buffers).  Round 5: with page-locking, a process
+// that registers, unregisters and frees a buffer and later makes a pageable copy into memory the heap hands back
+// from those pages can fault in that copy (hipErrorIllegalAddress; three closing-suite runs and a directed test,
+// even with every device synchronised around hipHostUnregister), and the host path is PCIe-bound
+// either way (64-65 GB/s staged or registered): locking is opt-in.
+std::atomic<int> g_host_lock{0};
+
+MTB_API int32_t gpu_set_host_locking(int32_t mode) {
+    if (mode != 0 && mode != 1) {
+        set_error("gpu_set_host_locking(%d): mode must be 0 (record only) or 1 (page-lock)", mode);
+        return MTB_BAD_ARGS;
+    }
+    return g_host_lock.exchange(mode);
+}
+
 MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
     if (!ptr || count <= 0) {
         set_error("gpu_register_host: null buffer or count %lld <= 0", (long long)count);
@@ -1535,8 +1551,9 @@ MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
     r.bytes = bytes;
     r.lo = (a + kHostPage - 1) & ~(kHostPage - 1);
     r.hi = (a + bytes) & ~(kHostPage - 1);
-    if (r.hi <= r.lo) {
-        r.lo = r.hi = 0;  // no whole page inside the buffer: nothing to lock, batches stage it (still registered)
+    if (r.hi <= r.lo || !g_host_lock.load()) {
+        r.lo = r.hi = 0;  // locking off, or no whole page inside the buffer: nothing locked, batches stage it (still
+                          // registered)
     } else {
         if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
             set_error("gpu_register_host: [%p, +%zu B) is already page-locked (hipHostMalloc / another registration)",

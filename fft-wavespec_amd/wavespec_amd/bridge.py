@@ -61,6 +61,7 @@ SIGNATURES = {
     "gpu_set_kalman_params": (C.c_int32, [_d, C.c_int32]),
     "gpu_register_host": (C.c_int32, [_d, C.c_int64]),
     "gpu_unregister_host": (C.c_int32, [_d]),
+    "gpu_set_host_locking": (C.c_int32, [C.c_int32]),
     "gpu_session_id": (C.c_int64, []),
     "gpu_spectrum_topk_batch": (C.c_int32, [_d, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                             C.c_int32, C.c_int32, C.c_double, C.c_double, _d, C.c_int32, _i32p]),
@@ -279,6 +280,15 @@ def unregister_host(a: np.ndarray) -> None:
     """gpu_unregister_host: raises on every failure -- an unknown buffer (BAD_ARGS) and a runtime that
     refused or still maps the range (INTERNAL_ERROR: the buffer stays page-locked and must not be freed)."""
     _check("gpu_unregister_host", lib().gpu_unregister_host(_dptr(a)))
+
+
+def set_host_locking(mode: int) -> int:
+    """gpu_set_host_locking: 1 = register_host page-locks the whole pages inside a buffer, 0 = it only records
+    the range (the default; calls stage).  Returns the previous mode."""
+    r = int(lib().gpu_set_host_locking(mode))
+    if r < 0:
+        _check("gpu_set_host_locking", r)
+    return r
 
 
 def session_id() -> int:

@@ -240,8 +240,8 @@ MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
  * gpu_submit_spectrum_batch still copies its input (1.1.0:1316).
  * Registrations belong to the session and end with it (last gpu_shutdown).
  *
- * Page granularity (round 5): only the whole pages INSIDE [ptr, ptr + count)
- * are page-locked -- the page-exact span [round_up(ptr, 4096),
+ * Page granularity (round 5; page-locking is opt-in, gpu_set_host_locking):
+ * only the whole pages INSIDE [ptr, ptr + count) are page-locked -- the page-exact span [round_up(ptr, 4096),
  * round_down(ptr + count, 4096)) -- never a page the buffer shares with other
  * memory; the < 1-page head and tail of the buffer go through a small pinned
  * bounce buffer of each call.  A buffer with no whole page inside is
@@ -259,6 +259,15 @@ MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
  * place (the buffer stays locked and must not be freed). */
 MTB_API int32_t gpu_register_host(const double *ptr, int64_t count);
 MTB_API int32_t gpu_unregister_host(const double *ptr);
+/* Whether gpu_register_host page-locks (mode 1) or only records the range
+ * (mode 0, the default: calls on a registered buffer stage through the
+ * library's pinned buffers -- the same results; the host path is PCIe-bound
+ * either way).  Round 5: with page-locking, a process that registers,
+ * unregisters and frees a buffer can later fault (hipErrorIllegalAddress) in a
+ * pageable copy into memory reused from those pages, ROCm 7.x.
+ * Affects later registrations only.  Returns the previous mode, or MTB_BAD_ARGS
+ * for a mode other than 0 / 1. */
+MTB_API int32_t gpu_set_host_locking(int32_t mode);
 /* The current session's identity: a number > 0 that changes whenever the
  * session is torn down (last gpu_shutdown) and a new one opened; 0 without a
  * session.  Registrations belong to one session: a caller that registered a

@@ -305,6 +305,11 @@ int main(int argc, char **argv) {
     sym(h, A.plan_destroy, "wsp_plan_destroy");
     sym(h, A.reg, "gpu_register_host");
     sym(h, A.unreg, "gpu_unregister_host");
+    {  // the page-locking form (opt-in since round 5): the fake runtime checks its page-exact spans
+        decltype(&gpu_set_host_locking) lock_mode = nullptr;
+        sym(h, lock_mode, "gpu_set_host_locking");
+        CHECK(lock_mode(1) == 0, "host locking was off by default");
+    }
     sym(h, A.group_create, "wsp_group_create");
     sym(h, A.group_execute, "wsp_group_execute");
     sym(h, A.group_set_mode, "wsp_group_set_mode");

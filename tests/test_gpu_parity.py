@@ -727,8 +727,9 @@ def test_kalman_params(gpu_session, prec, kw):
 
 
 def test_register_host_direct_dma(gpu_session):
-    """gpu_register_host: a registered fp64 series is DMA'd in place and a registered output array
-    receives the results directly (no staging copy); results identical to the staged path."""
+    """gpu_register_host (default mode: the ranges are recorded, calls stage): a registered fp64 series and output
+    array give results identical to the unregistered path, views inside the series are covered, overlapping and
+    unknown ranges are refused.  (The page-locking form with in-place DMA: test_host_locking_opt_in.)"""
     n, hop = 1024, 256
     s = synth.random_walk(300 * hop + n, seed=41)
     nwin = 1 + (s.size - n) // hop
@@ -810,11 +811,10 @@ def _hip_knows(addr: int) -> bool:
 
 
 def test_register_host_page_edges(gpu_session):
-    """Round 5: only the whole pages inside a registered buffer are page-locked.
-    Buffers that start and end mid-page, share pages with each other and with unregistered memory, and one
-    with no whole page inside: the batch results equal the staged path's, the runtime maps exactly the inner
-    pages while registered and nothing after unregistering, and a registration over an already registered
-    buffer's pages is refused."""
+    """Round 5: registering buffers that start and end mid-page and share pages with each other
+    and with unregistered memory, in the default mode (gpu_set_host_locking(0): the range is recorded, nothing is
+    page-locked, calls stage): the runtime maps none of it, the batch results equal the staged path's, an
+    overlapping registration is refused, and a buffer with no whole page inside registers as well."""
     page = 4096
     n, hop = 512, 7
     arena = np.zeros((16 << 20) // 8)  # one allocation holding several neighbouring arrays
@@ -832,11 +832,10 @@ def test_register_host_page_edges(gpu_session):
     try:
         lo = -(-s.ctypes.data // page) * page
         hi = (s.ctypes.data + s.nbytes) // page * page
-        assert _hip_knows(lo) and _hip_knows(hi - 1)
-        assert not _hip_knows(lo - 1) and not _hip_knows(hi)  # the shared head / tail pages stay pageable
+        assert not _hip_knows(lo) and not _hip_knows(hi - 1)  # recorded only: nothing page-locked
         p = bridge.spectrum_batch(s, n, hop, "mean", "hann", out=out)
         assert np.shares_memory(p, out) and np.array_equal(p, staged)
-        sub = s[1001:-333]  # a view that starts and ends mid-page inside the registered span
+        sub = s[1001:-333]  # a view that starts and ends mid-page inside the registered range
         assert np.array_equal(gpu(sub, n, hop, "mean", "hann"), gpu(sub.copy(), n, hop, "mean", "hann"))
         with pytest.raises(bridge.BridgeError) as e:
             bridge.register_host(s[5:9])
@@ -845,20 +844,31 @@ def test_register_host_page_edges(gpu_session):
     finally:
         bridge.unregister_host(out)
         bridge.unregister_host(s)
-    assert not _hip_knows(lo) and not _hip_knows(hi - 1)
-    tiny = arena[first + 3:first + 300]  # no whole page inside: registered, nothing locked, batches stage
+    tiny = arena[first + 3:first + 300]
     bridge.register_host(tiny)
     try:
-        assert not _hip_knows(tiny.ctypes.data)
         assert np.array_equal(gpu(tiny, 64, 5), gpu(tiny.copy(), 64, 5))
     finally:
         bridge.unregister_host(tiny)
 
 
+def test_host_locking_opt_in(gpu_session):
+    """gpu_set_host_locking(1): registrations page-lock exactly the whole pages inside the buffer (the shared head /
+    tail pages stay pageable), results equal the staged path's, overlap is refused and nothing stays mapped after
+    unregistering.  Run in a child process (tests/host_locking_child.py): after a page-locked buffer is unregistered
+    and freed, a later pageable copy into reused pages can fault on this runtime, and the child's
+    runtime state ends with it."""
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "host_locking_child.py")], capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-2000:], r.stderr[-4000:])
+    assert bridge.set_host_locking(0) == 0  # this process never switched it on
+
+
 def test_pageable_copies_after_registrations(gpu_session):
-    """The round-4 fault sequence (profiles/r04/faults): numpy arrays registered and unregistered, freed, and
-    then pageable device-to-host and host-to-device copies through torch into freshly allocated host memory
-    of many sizes (the heap then reuses the freed pages) -- every byte must arrive."""
+    """The round-4 / round-5 fault sequence (profiles/r04/faults, profiles/r05/faults): numpy arrays registered and
+    unregistered, freed, and then pageable device-to-host and host-to-device copies through torch into freshly
+    allocated host memory of many sizes (the heap then reuses the freed pages) -- every byte must arrive.  With
+    page-locking this faulted in the copies (r05diag2, r05final3); in the default mode it must not."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     for r in range(6):
