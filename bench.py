@@ -308,10 +308,12 @@ class Workload:
 
 
 C5_BARS, C5_LENS = 20000, (512, 1024, 2048, 4096)
-# C5 cost per window of each length for --c5-shard split-time: the round-3 kernel trace of the grouped plan
-# (profiles/r03/c5_kernel_stats.csv: 374 / 235 / 122 / 69 us for the 4096 / 2048 / 1024 / 512 launches over
-# 7 symbols each), in units of 10 ps per window; output bytes alone (N / 2) undercount the short windows
-C5_TIME_WEIGHTS = {512: 51, 1024: 92, 2048: 187, 4096: 336}
+# C5 cost per window of each length for --c5-shard split-time, in units of 10 ps per window: round 5 calibrated them at
+# shard scale from the G = 8 emulation of the final tree (profiles/r05/shards.json, ranks holding one or two lengths
+# solved for per-window times: 0.48 / 0.96 / 1.94 / 4.14 ns) -- a 4096-point window costs ~7 % more per output byte
+# than the shorter ones at one round of tasks (its seed is the longest); round 3's whole-batch kernel trace gave
+# {512: 51, 1024: 92, 2048: 187, 4096: 336}
+C5_TIME_WEIGHTS = {512: 48, 1024: 96, 2048: 194, 4096: 414}
 
 
 def c5_symbols():
