@@ -129,9 +129,8 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, 2) void inverse_kernel(const dou
 // hits the line the first brought into L2 (in natural order 0.3 of the second reads went to HBM: PMC 2.79 GB of
 // reads per step against 2.15 GB algorithmic, profiles/r04/inverse_*); variant 3 keeps the natural order.
 // NTS: non-temporal sample stores (the default); variant 4 = plain stores (a pure write stream ran 5.75 TB/s with
-// plain 16-B stores against 5.5 with non-temporal ones, profiles/r02/slide/write_probe.log).  WTS (variant 5):
-// write-through (sc1) sample stores; NTL (variant 6): non-temporal spectrum loads (A/B, round 5).
-template <int LOG2N, int SPLIT, bool PAIRED = true, bool NTS = true, bool WTS = false, bool NTL = false>
+// plain 16-B stores against 5.5 with non-temporal ones, profiles/r02/slide/write_probe.log).
+template <int LOG2N, int SPLIT, bool PAIRED = true, bool NTS = true>
 __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_direct_kernel(
     const double *__restrict__ in, double *__restrict__ out, const cpx<double> *__restrict__ tw, int64_t n_windows,
     int64_t n_groups) {
@@ -160,10 +159,8 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_dire
             for (int i = 0; i < R0; ++i) {
                 const int r = PAIRED ? ((i & 1) ? R0 - 1 - (i >> 1) : (i >> 1)) : i;
                 const int k = (t + TPW * q) + (M / R0) * r;
-                const v2 *qa = reinterpret_cast<const v2 *>(xin + 2 * k);
-                const v2 *qb = reinterpret_cast<const v2 *>(xin + 2 * ((M - k) & (M - 1)));
-                const v2 pa = NTL ? __builtin_nontemporal_load(qa) : *qa;
-                const v2 pb = NTL ? __builtin_nontemporal_load(qb) : *qb;
+                const v2 pa = *reinterpret_cast<const v2 *>(xin + 2 * k);
+                const v2 pb = *reinterpret_cast<const v2 *>(xin + 2 * ((M - k) & (M - 1)));
                 // k = 0 only for t = 0 at (q, r) = (0, 0): real DC, X_M = 0 (branch-free selects)
                 const bool dc = (q == 0 && r == 0) && k == 0;
                 const cpx<T> xa = {pa.x, dc ? T(0) : pa.y};
@@ -200,16 +197,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::BLOCK, SPLIT ? 3 : 2) void inverse_dire
             for (int r = 0; r < 8; ++r) {
                 const v2 a = {u0[r].re * kScale, -u0[r].im * kScale}, b = {u1[r].re * kScale, -u1[r].im * kScale};
                 v2 *pa = reinterpret_cast<v2 *>(xo + 2 * (bq0 + B * r)), *pb = reinterpret_cast<v2 *>(xo + 2 * (bq1 + B * r));
-                if constexpr (WTS) {
-                    // sc1 buffer stores, 16 B per lane as the plain form; descriptor at the group's first window
-                    const __amdgpu_buffer_rsrc_t orc =
-                        __builtin_amdgcn_make_buffer_rsrc(out + g * WPB * (int64_t)N, (short)0, 0x7fffffff, 0x00020000);
-                    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, a), orc,
-                                                           (int)((slot * N + 2 * (bq0 + B * r)) * (int)sizeof(T)), 0, 16);
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, b), orc,
-                                                           (int)((slot * N + 2 * (bq1 + B * r)) * (int)sizeof(T)), 0, 16);
-                } else if constexpr (NTS) {
+                if constexpr (NTS) {
                     __builtin_nontemporal_store(a, pa);
                     __builtin_nontemporal_store(b, pb);
                 } else {
@@ -309,12 +297,6 @@ hipError_t launch_inverse(const InverseLaunch &L, hipStream_t stream) {
         else if (L.variant == 4)                                                                              \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, true, false>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, \
                                stream, L.in, L.out, tw, L.n_windows, groups);                                 \
-        else if (L.variant == 5)                                                                              \
-            hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, true, true, true>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), \
-                               0, stream, L.in, L.out, tw, L.n_windows, groups);                              \
-        else if (L.variant == 6)                                                                              \
-            hipLaunchKernelGGL((inverse_direct_kernel<LG, 2, true, true, false, true>), dim3((unsigned)grid),        \
-                               dim3(Geo<LG>::BLOCK), 0, stream, L.in, L.out, tw, L.n_windows, groups);        \
         else                                                                                                  \
             hipLaunchKernelGGL((inverse_direct_kernel<LG, 2>), dim3((unsigned)grid), dim3(Geo<LG>::BLOCK), 0, stream, L.in, \
                                L.out, tw, L.n_windows, groups);                                               \

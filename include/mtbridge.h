@@ -374,8 +374,7 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
  *    with the AoS exchange; 3 = 0 with the element loads in natural order
- *    (round 4); 4 = 0 with plain (not non-temporal) sample stores, 5 = with
- *    write-through (sc1) ones, 6 = with non-temporal spectrum loads; 0 = the
+ *    (round 4); 4 = 0 with plain (not non-temporal) sample stores; 0 = the
  *    pre-step in registers, split exchange, each element's two reads (as X_k
  *    and as a mirror X_(M-k)) one load step apart;
  *  - MTB_OUT_PHASE records at N = 2048 / 4096 without IIR detrend: 2 = the
