@@ -112,6 +112,20 @@ def test_unknown_job_and_plan():
     assert bridge.lib().wsp_plan_algorithmic_bytes(987654321) == -1
 
 
+def test_host_locking_mode():
+    """gpu_set_host_locking: record-only (0) by default, returns the previous mode, refuses anything but 0 / 1
+    (no session needed: it only selects what later registrations do)."""
+    L = bridge.lib()
+    assert L.gpu_set_host_locking(2) == bridge.BAD_ARGS
+    assert L.gpu_set_host_locking(-1) == bridge.BAD_ARGS
+    assert bridge.set_host_locking(1) == 0
+    assert bridge.set_host_locking(1) == 1
+    assert bridge.set_host_locking(0) == 1
+    assert bridge.set_host_locking(0) == 0
+    with pytest.raises(bridge.BridgeError):
+        bridge.set_host_locking(7)
+
+
 @pytest.mark.skipif(GPU, reason="checks the no-GPU behaviour")
 def test_no_gpu_fails_loudly_without_fallback():
     assert bridge.lib().gpu_init(0, 64) == bridge.BACKEND_UNAVAILABLE
