@@ -562,6 +562,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             K.n_windows = c.n_windows;
             K.n = c.n;
             K.f32 = c.f32;
+            K.variant = c.variant;  // the plan's Kalman pre-pass forms (wsp_plan_set_variant: 1, 2, 7)
             memcpy(K.params, kalman, sizeof(K.params));
             HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
             G.series = wsb + ws.det;
@@ -702,91 +703,18 @@ struct LiveCtx {
     }
 };
 
-// Caller buffers page-locked by gpu_register_host (north star: "FeedCache.mqh rewired to stage
-// price bars into pinned host buffers for hipMemcpyAsync").  A registered fp64 series is DMA'd to
-// the device from where it lies, and a registered output array receives the D2H copy directly:
-// no staging copy on either side of a synchronous batch.  Held by the session, released with it.
-//
-// Only WHOLE PAGES INSIDE the caller's buffer are page-locked (round 5): [a, a + bytes) registers
-// [round_up(a), round_down(a + bytes)), page-exact, and the < 1-page head and tail outside that span go
-// through a small pinned bounce buffer per batch.  A caller's heap array shares its first and last page
-// with other heap objects; page-locking those pages (which hipHostRegister does for any byte range, the
-// pinning granularity is the page) left the runtime holding host-pointer mappings over memory the
-// library does not own, and page-sharing registrations of neighbouring arrays overlapped in those pages
-// (the round-4 illegal-address faults).  With page-exact spans inside disjoint caller
-// buffers no page is ever locked that holds anything but the registered array, no two registrations
-// share a page, and the span unregistered is exactly the span registered.
-constexpr uintptr_t kHostPage = 4096;
-struct HostRegion {
-    size_t bytes = 0;       // the caller's range [base, base + bytes)
-    uintptr_t lo = 0, hi = 0;  // page-locked span [lo, hi), page-aligned, inside the caller's range; empty: nothing locked
-};
-// The part of a host range that can be DMA'd in place: [lo, hi) inside [p, p + n), page-locked.
-struct HostSpan {
-    const char *p = nullptr;
-    size_t n = 0;
-    uintptr_t lo = 0, hi = 0;
-    bool direct() const { return hi > lo; }
-    size_t head() const { return direct() ? (size_t)(lo - (uintptr_t)p) : n; }   // bytes before the span
-    size_t tail() const { return direct() ? (size_t)((uintptr_t)p + n - hi) : 0; }  // bytes after it
-};
+// Caller buffers registered by gpu_register_host (north star: "FeedCache.mqh rewired to stage price bars into
+// pinned host buffers for hipMemcpyAsync").  Round 6: the library never page-locks caller memory.  A registration
+// records the range (refusing overlaps) and nothing else; every call stages through the library's own pinned
+// buffers -- the input through pinned staging, a synchronous call's output through a pinned ring drained while
+// later parts are still copied off the device (batch_ring_out).  Page-locking the caller's array (hipHostRegister)
+// was opt-in in round 5 and is withdrawn: after such an array was unregistered and freed, a later pageable copy
+// into memory reused from its pages could fault (hipErrorIllegalAddress) inside the runtime, with every device
+// synchronised around hipHostUnregister.  No exported mode can reach that sequence now.
 struct HostRegistry {
     std::mutex mu;
-    std::map<uintptr_t, HostRegion> regions;  // caller base -> region, caller ranges disjoint
-    // [p, p + bytes) inside one registered caller range: its page-locked part (empty span otherwise)
-    HostSpan span(const void *p, size_t bytes) {
-        HostSpan s;
-        s.p = static_cast<const char *>(p);
-        s.n = bytes;
-        if (!p || !bytes) return s;
-        const uintptr_t a = (uintptr_t)p;
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = regions.upper_bound(a);
-        if (it == regions.begin()) return s;
-        --it;
-        if (a < it->first || a + bytes > it->first + it->second.bytes || it->second.hi <= it->second.lo) return s;
-        s.lo = std::max(a, it->second.lo);
-        s.hi = std::min(a + bytes, it->second.hi);
-        if (s.hi <= s.lo) s.lo = s.hi = 0;
-        return s;
-    }
-    ~HostRegistry() {
-        for (auto &r : regions)
-            if (r.second.hi > r.second.lo) (void)hipHostUnregister((void *)r.second.lo);
-    }
+    std::map<uintptr_t, size_t> regions;  // caller base -> bytes, caller ranges disjoint
 };
-
-// Does the HIP runtime map host address p as page-locked memory?  (hipPointerGetAttributes: registered
-// and pinned host memory report hipMemoryTypeHost; pageable memory an error or hipMemoryTypeUnregistered.)
-bool hip_knows_host(const void *p) {
-    hipPointerAttribute_t a;
-    memset(&a, 0, sizeof(a));
-    const hipError_t e = hipPointerGetAttributes(&a, p);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();  // a failed query is the expected answer for pageable memory: clear it
-        return false;
-    }
-    return a.type != hipMemoryTypeUnregistered;
-}
-
-// Host <-> device copies of the byte range [off, off + len) of a caller range whose page-locked part is `s`:
-// the page-locked part straight from / to the caller's memory, the head and tail (< 1 page each) from / to
-// `bounce` (pinned: head at bounce[0, 4096), tail at bounce[4096, 8192)).  h2d: dev <- host.
-hipError_t span_copy(const HostSpan &s, char *bounce, size_t off, size_t len, void *dev, bool h2d, hipStream_t st) {
-    const size_t h = s.head(), t0 = s.n - s.tail();
-    const size_t cut[4] = {0, h, t0, s.n};
-    for (int piece = 0; piece < 3; ++piece) {
-        const size_t b0 = std::max(off, cut[piece]), b1 = std::min(off + len, cut[piece + 1]);
-        if (b1 <= b0) continue;
-        char *host = piece == 1 ? const_cast<char *>(s.p) + b0
-                                : bounce + (piece == 0 ? b0 : kHostPage + (b0 - t0));
-        char *d = static_cast<char *>(dev) + (b0 - off);
-        const hipError_t e = h2d ? hipMemcpyAsync(d, host, b1 - b0, hipMemcpyHostToDevice, st)
-                                 : hipMemcpyAsync(host, d, b1 - b0, hipMemcpyDeviceToHost, st);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
 
 struct Session {
     int device_index = 0;
@@ -794,7 +722,7 @@ struct Session {
     std::vector<std::unique_ptr<DeviceCtx>> devs;
     std::mutex live_mu;
     std::vector<std::unique_ptr<LiveCtx>> live_free;
-    HostRegistry host_regs;  // destroyed before devs (declared after): unregistered while the contexts live
+    HostRegistry host_regs;  // recorded caller ranges (gpu_register_host); nothing of the caller is page-locked
 };
 
 // Session lifetime (SURVEY 8b "per-session refcount"): every successful
@@ -831,19 +759,17 @@ struct Batch {
     Config cfg;
     double kalman[16];
     std::vector<Part> parts;
-    void *h_in = nullptr, *h_out = nullptr;  // pinned staging (null when the caller's buffer is registered)
+    void *h_in = nullptr, *h_out = nullptr;  // pinned staging (h_out: async jobs; synchronous calls use the ring)
     size_t h_in_bytes = 0, h_out_bytes = 0;
-    double *direct_out = nullptr;            // registered caller output receiving the D2H copies
-    HostSpan in_span, out_span;              // page-locked parts of the caller's series / output (direct paths)
-    char *bounce = nullptr;                  // pinned: series head / tail [0, 8 KiB), output head / tail [8, 16 KiB)
-    static constexpr size_t kBounce = 4 * kHostPage;
+    std::vector<void *> ring;                // synchronous calls: pinned output slots, part i -> ring[i % size]
+    size_t ring_bytes = 0;
     int status = MTB_OK;
     std::string error;
     ~Batch() {
         for (auto &p : parts) {
             (void)hipSetDevice(p.dev);
             if (p.recorded) (void)hipEventSynchronize(p.done);
-            else if (p.stream) (void)hipStreamSynchronize(p.stream);  // a part abandoned mid-enqueue
+            else if (p.stream) (void)hipStreamSynchronize(p.stream);  // a part abandoned mid-enqueue / not copied out
             event_free(p.dev, p.done);
             dev_free(p.dev, p.d_in, p.in_bytes);
             dev_free(p.dev, p.d_out, p.out_bytes);
@@ -851,7 +777,7 @@ struct Batch {
         }
         host_free(h_in, h_in_bytes);
         host_free(h_out, h_out_bytes);
-        host_free(bounce, kBounce);
+        for (void *r : ring) host_free(r, ring_bytes);
     }
 };
 
@@ -896,15 +822,20 @@ void stage_out(double *dst, const void *src, int64_t n, bool f32) {  // pinned r
 
 // Stages `series` (double, chronological) and enqueues every part.  A batch
 // is cut into parts: contiguous window ranges per device (the multi-GPU
-// shard), each cut again into up to 16 chunks of >= 64 MiB of input on the
-// device's streams, so that the host staging of chunk i+1, the H2D copy, the
-// kernels and the D2H copy of earlier chunks overlap.  Each part copies its
-// own input slice (with the N - hop halo of overlapping windows).
-// `out_direct` (synchronous calls only): the caller's output array, used as the D2H destination
-// when it is registered, holds every record and the plan is fp64; the series likewise goes
-// straight from a registered buffer (fp32 plans convert, so they always stage).
-int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out,
-                double *out_direct = nullptr) {
+// shard), each cut again into chunks on the device's streams, so that the
+// host staging of chunk i+1, the H2D copy, the kernels and the D2H copy of
+// earlier chunks overlap.  Each part copies its own input slice (with the
+// N - hop halo of overlapping windows).
+// `ring` (synchronous calls): the parts are cut by input AND output bytes (>= 64 MiB each, up to 64 per
+// device) and their results are not copied off the device here: batch_ring_out moves them through a few
+// pinned slots, draining one into the caller's array while the next ones are in flight -- so an output-
+// dominated call (C4 from host memory: 8.4 MB in, 8 GiB out) overlaps its host copy-out with the PCIe
+// transfer and holds a few hundred MiB of pinned memory instead of the whole result.  Asynchronous jobs
+// (gpu_submit_spectrum_batch) keep the whole result in pinned staging until the caller polls.
+#ifndef WSP_PART_BYTES
+#define WSP_PART_BYTES (64 << 20)  // the sanitizer builds (tests/hostsan) cut at 64 KiB to exercise many parts
+#endif
+int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out, bool ring = false) {
     auto b = std::make_unique<Batch>();
     b->cfg = c;
     {
@@ -914,30 +845,19 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
     const size_t es = c.elem();
     const int64_t in_elems = c.series_elems();
     const size_t in_bytes = (size_t)in_elems * es, out_bytes = (size_t)(c.n_windows * c.record()) * es;
-    if (!c.f32) b->in_span = S.host_regs.span(series, in_bytes);
-    if (!c.f32 && out_direct) b->out_span = S.host_regs.span(out_direct, out_bytes);
-    const bool din = b->in_span.direct();
-    if (b->out_span.direct()) b->direct_out = out_direct;
-    if (din || b->direct_out) {  // the < 1-page head / tail of a registered caller range go through here
-        if (!(b->bounce = static_cast<char *>(host_alloc(Batch::kBounce)))) return MTB_NO_MEM;
-        if (din) {
-            const HostSpan &s = b->in_span;
-            memcpy(b->bounce, s.p, s.head());
-            memcpy(b->bounce + kHostPage, s.p + s.n - s.tail(), s.tail());
-        }
-    }
-    if (!din) {
-        b->h_in_bytes = in_bytes;
-        if (!(b->h_in = host_alloc(in_bytes))) return MTB_NO_MEM;
-    }
-    if (!b->direct_out) {
+    b->h_in_bytes = in_bytes;
+    if (!(b->h_in = host_alloc(in_bytes))) return MTB_NO_MEM;
+    if (!ring) {
         b->h_out_bytes = out_bytes;
         if (!(b->h_out = host_alloc(out_bytes))) return MTB_NO_MEM;
     }
     const int G = (int)std::min<int64_t>((int64_t)S.devs.size(), c.n_windows);
     const int64_t per_dev = (c.n_windows + G - 1) / G;
-    const int64_t dev_bytes = std::max<int64_t>(1, (per_dev - 1) * c.hop + c.n) * (int64_t)es;
-    const int64_t K = std::max<int64_t>(1, std::min<int64_t>({int64_t(16), dev_bytes / (int64_t(64) << 20), per_dev}));
+    const int64_t dev_in = std::max<int64_t>(1, (per_dev - 1) * c.hop + c.n) * (int64_t)es;
+    const int64_t dev_out = per_dev * c.record() * (int64_t)es;
+    const int64_t cut_bytes = ring ? std::max(dev_in, dev_out) : dev_in;
+    const int64_t K = std::max<int64_t>(1, std::min<int64_t>({ring ? int64_t(64) : int64_t(16),
+                                                              cut_bytes / (int64_t)WSP_PART_BYTES, per_dev}));
     const int64_t per = (per_dev + K - 1) / K;
     int64_t staged = 0;  // series elements already in the pinned buffer
     for (int g = 0; g < G; ++g) {
@@ -964,28 +884,19 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             P.done = event_alloc(P.dev);
             if (!P.done) return MTB_INTERNAL_ERROR;
             const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
-            if (!din && e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
+            if (e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
                 stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
                 staged = e1;
             }
-            if (din) {
-                HIP_OR(span_copy(b->in_span, b->bounce, (size_t)e0 * es, P.in_bytes, P.d_in, true, P.stream),
-                       MTB_INTERNAL_ERROR);
-            } else {
-                HIP_OR(hipMemcpyAsync(P.d_in, (const char *)b->h_in + (size_t)e0 * es, P.in_bytes, hipMemcpyHostToDevice,
-                                      P.stream),
-                       MTB_INTERNAL_ERROR);
-            }
+            HIP_OR(hipMemcpyAsync(P.d_in, (const char *)b->h_in + (size_t)e0 * es, P.in_bytes, hipMemcpyHostToDevice,
+                                  P.stream),
+                   MTB_INTERNAL_ERROR);
             int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
             if (st != MTB_OK) return st;
+            if (ring) continue;  // copied off the device by batch_ring_out
             const size_t o0 = (size_t)(P.w0 * c.record()) * es;
-            if (b->direct_out) {
-                HIP_OR(span_copy(b->out_span, b->bounce + 2 * kHostPage, o0, P.out_bytes, P.d_out, false, P.stream),
-                       MTB_INTERNAL_ERROR);
-            } else {
-                HIP_OR(hipMemcpyAsync((char *)b->h_out + o0, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream),
-                       MTB_INTERNAL_ERROR);
-            }
+            HIP_OR(hipMemcpyAsync((char *)b->h_out + o0, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream),
+                   MTB_INTERNAL_ERROR);
             HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
             P.recorded = true;
         }
@@ -1015,8 +926,7 @@ int batch_poll(Batch &b, bool wait) {
 }
 
 // Copies finished records (converted to double) into the caller's buffer;
-// with `wait`, part by part as each one completes (the copy-out of early
-// parts overlaps the D2H of later ones).
+// with `wait`, part by part as each one completes.
 int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int32_t *n_out) {
     const int64_t rec = b.cfg.record();
     const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
@@ -1026,16 +936,56 @@ int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int3
             const int st = part_poll(p, true);
             if (st != MTB_OK) return st;
         }
-        if (b.direct_out) continue;  // the D2H copies already landed in the caller's registered array
         const int64_t r1 = std::min<int64_t>(p.w0 + p.nw, nrec);
         stage_out(out + p.w0 * rec, (const char *)b.h_out + (size_t)(p.w0 * rec) * b.cfg.elem(), (r1 - p.w0) * rec,
                   b.cfg.f32);
     }
-    if (b.direct_out && wait) {  // every part done: the head / tail of the caller's array from the bounce buffer
-        const HostSpan &s = b.out_span;
-        char *o = reinterpret_cast<char *>(b.direct_out);
-        memcpy(o, b.bounce + 2 * kHostPage, s.head());
-        memcpy(o + s.n - s.tail(), b.bounce + 3 * kHostPage, s.tail());
+    *n_out = (int32_t)nrec;
+    return MTB_OK;
+}
+
+// Synchronous copy-out through the pinned ring (batch_start(ring = true)): the records of part i go device ->
+// ring[i % R] on the part's stream (after its kernel), and while the host drains slot i into the caller's array
+// the D2H copies of parts i+1 .. i+R-1 are in flight; slot i is refilled (part i+R) as soon as it is drained.
+// Only the parts holding records below out_cap are copied.
+constexpr int kRingSlots = 4;
+int batch_ring_out(Batch &b, double *out, int64_t out_cap, int32_t *n_out) {
+    const int64_t rec = b.cfg.record();
+    const size_t es = b.cfg.elem();
+    const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
+    int np = 0;
+    size_t slot = 0;
+    for (const auto &p : b.parts) {
+        if (p.w0 >= nrec) break;
+        ++np;
+        slot = std::max(slot, p.out_bytes);
+    }
+    const int R = std::min(kRingSlots, np);
+    b.ring_bytes = slot;
+    for (int r = 0; r < R; ++r) {
+        b.ring.push_back(host_alloc(slot));
+        if (!b.ring.back()) return MTB_NO_MEM;
+    }
+    auto nrec_of = [&](const Part &p) { return std::min<int64_t>(p.w0 + p.nw, nrec) - p.w0; };
+    auto issue = [&](int i) -> int {
+        Part &P = b.parts[i];
+        HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
+        HIP_OR(hipMemcpyAsync(b.ring[i % R], P.d_out, (size_t)(nrec_of(P) * rec) * es, hipMemcpyDeviceToHost, P.stream),
+               MTB_INTERNAL_ERROR);
+        HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+        P.recorded = true;
+        return MTB_OK;
+    };
+    for (int i = 0; i < R; ++i) {
+        const int st = issue(i);
+        if (st != MTB_OK) return st;
+    }
+    for (int i = 0; i < np; ++i) {
+        const Part &P = b.parts[i];
+        int st = part_poll(P, true);
+        if (st != MTB_OK) return st;
+        stage_out(out + P.w0 * rec, b.ring[i % R], nrec_of(P) * rec, b.cfg.f32);
+        if (i + R < np && (st = issue(i + R)) != MTB_OK) return st;
     }
     *n_out = (int32_t)nrec;
     return MTB_OK;
@@ -1048,11 +998,10 @@ int run_sync(const Config &c, const double *series, double *out, int64_t out_cap
         return MTB_BACKEND_UNAVAILABLE;
     }
     std::unique_ptr<Batch> b;
-    const bool whole = out_cap >= c.n_windows * c.record();  // a truncated request never lands directly
-    int st = batch_start(*S, c, series, &b, whole ? out : nullptr);
+    int st = batch_start(*S, c, series, &b, true);
     if (st != MTB_OK) return st;
     int32_t n = 0;
-    st = batch_copy_out(*b, out, out_cap, true, &n);
+    st = batch_ring_out(*b, out, out_cap, &n);
     if (st != MTB_OK) return st;
     if (out_len) *out_len = n;
     return MTB_OK;
@@ -1242,10 +1191,9 @@ struct Group {
     int mode = 0;
     int *ctr = nullptr;                    // 256 task-counter slots (counter, done) on the device, zeroed at create
     uint32_t exec_no = 0;
-    // per slot: the event its last execute recorded and that execute's stream -- an execute on another stream
-    // waits for the slot's previous user before it reuses the counters (more than 256 executes in flight)
+    // per slot: the event its last execute recorded -- every execute waits for the slot's previous user before
+    // it reuses the counters (more than 256 executes in flight; a no-op on the same stream)
     std::vector<hipEvent_t> slot_ev;
-    std::vector<hipStream_t> slot_st;
     long long *trace = nullptr;            // wsp_group_set_trace: diagnostic per-task timeline of the mixed launch
     int64_t trace_cap = 0, last_tasks = 0;
     // wsp_group_set_streams(n > 1): n - 1 internal streams beside the caller's (wsp_group_execute)
@@ -1381,17 +1329,13 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     const int slot = (int)(g.exec_no++ % kMixSlots);
     m.counter = g.ctr + 2 * slot;
     m.done = g.ctr + 2 * slot + 1;
-    if (g.slot_ev.empty()) {
-        g.slot_ev.assign(kMixSlots, nullptr);
-        g.slot_st.assign(kMixSlots, nullptr);
-    }
+    if (g.slot_ev.empty()) g.slot_ev.assign(kMixSlots, nullptr);
     hipEvent_t &ev = g.slot_ev[slot];
     if (!ev) HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), MTB_INTERNAL_ERROR);
-    else if (g.slot_st[slot] != s) HIP_OR(hipStreamWaitEvent(s, ev, 0), MTB_INTERNAL_ERROR);  // same stream: in order
+    else HIP_OR(hipStreamWaitEvent(s, ev, 0), MTB_INTERNAL_ERROR);  // always: a destroyed stream's handle can come back
     const int grid = (int)std::min<int64_t>(res, tasks);
     HIP_OR(launch_slide_mix(m, nf, det, c0.f32, grid, s), MTB_INTERNAL_ERROR);
     HIP_OR(hipEventRecord(ev, s), MTB_INTERNAL_ERROR);
-    g.slot_st[slot] = s;
     return MTB_OK;
 }
 
@@ -1505,20 +1449,21 @@ MTB_API void gpu_shutdown(void) {
     }
 }
 
-// gpu_set_host_locking: whether gpu_register_host page-locks the caller's memory (1) or only records the range (0,
-// the default: batches on it stage through the library's pinned buffers).  Round 5: with page-locking, a process
-// that registers, unregisters and frees a buffer and later makes a pageable copy into memory the heap hands back
-// from those pages can fault in that copy (hipErrorIllegalAddress; three closing-suite runs and a directed test,
-// even with every device synchronised around hipHostUnregister), and the host path is PCIe-bound
-// either way (64-65 GB/s staged or registered): locking is opt-in.
-std::atomic<int> g_host_lock{0};
-
+// gpu_set_host_locking: round 5 made page-locking of caller memory opt-in (mode 1); round 6 withdraws it.
+// Mode 0 (record the range, stage through the library's pinned buffers) is the only mode: 0 returns 0, 1 is
+// refused with MTB_BAD_ARGS and an explanation, anything else is refused as before.  See HostRegistry.
 MTB_API int32_t gpu_set_host_locking(int32_t mode) {
-    if (mode != 0 && mode != 1) {
-        set_error("gpu_set_host_locking(%d): mode must be 0 (record only) or 1 (page-lock)", mode);
+    if (mode == 1) {
+        set_error("gpu_set_host_locking(1): page-locking caller memory was withdrawn (a pageable copy into pages of an "
+                  "unregistered, freed buffer could fault, DESIGN.md 4.2); registrations record the range and calls "
+                  "stage through the library's pinned buffers");
         return MTB_BAD_ARGS;
     }
-    return g_host_lock.exchange(mode);
+    if (mode != 0) {
+        set_error("gpu_set_host_locking(%d): mode must be 0 (record only)", mode);
+        return MTB_BAD_ARGS;
+    }
+    return 0;
 }
 
 MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
@@ -1533,47 +1478,20 @@ MTB_API int32_t gpu_register_host(const double *ptr, int64_t count) {
     }
     const uintptr_t a = (uintptr_t)ptr;
     const size_t bytes = (size_t)count * sizeof(double);
-    if (a + bytes < a) {
-        set_error("gpu_register_host: [%p, +%zu B) wraps the address space", (const void *)ptr, bytes);
+    if ((size_t)count > SIZE_MAX / sizeof(double) || a + bytes < a) {
+        set_error("gpu_register_host: [%p, +%lld doubles) wraps the address space", (const void *)ptr, (long long)count);
         return MTB_BAD_ARGS;
     }
     HostRegistry &R = S->host_regs;
     std::lock_guard<std::mutex> lk(R.mu);
-    // caller ranges are disjoint (so are the page-locked spans inside them: no page is locked twice)
-    auto it = R.regions.lower_bound(a);
+    auto it = R.regions.lower_bound(a);  // caller ranges are disjoint
     const bool overlaps = (it != R.regions.end() && it->first < a + bytes) ||
-                          (it != R.regions.begin() && std::prev(it)->first + std::prev(it)->second.bytes > a);
+                          (it != R.regions.begin() && std::prev(it)->first + std::prev(it)->second > a);
     if (overlaps) {
         set_error("gpu_register_host: [%p, +%zu B) overlaps a registered buffer", (const void *)ptr, bytes);
         return MTB_BAD_ARGS;
     }
-    HostRegion r;
-    r.bytes = bytes;
-    r.lo = (a + kHostPage - 1) & ~(kHostPage - 1);
-    r.hi = (a + bytes) & ~(kHostPage - 1);
-    if (r.hi <= r.lo || !g_host_lock.load()) {
-        r.lo = r.hi = 0;  // locking off, or no whole page inside the buffer: nothing locked, batches stage it (still
-                          // registered)
-    } else {
-        if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
-            set_error("gpu_register_host: [%p, +%zu B) is already page-locked (hipHostMalloc / another registration)",
-                      (const void *)ptr, bytes);
-            return MTB_BAD_ARGS;
-        }
-        const hipError_t e = hipHostRegister((void *)r.lo, r.hi - r.lo, hipHostRegisterPortable);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            set_error("hipHostRegister(%p, %zu bytes): %s", (void *)r.lo, (size_t)(r.hi - r.lo), hipGetErrorString(e));
-            return MTB_INTERNAL_ERROR;
-        }
-        if (!hip_knows_host((const void *)r.lo) || !hip_knows_host((const void *)(r.hi - 1))) {
-            (void)hipHostUnregister((void *)r.lo);
-            set_error("gpu_register_host: HIP does not report [%p, %p) as page-locked after hipHostRegister",
-                      (void *)r.lo, (void *)r.hi);
-            return MTB_INTERNAL_ERROR;
-        }
-    }
-    R.regions.emplace(a, r);
+    R.regions.emplace(a, bytes);
     return MTB_OK;
 }
 
@@ -1594,44 +1512,6 @@ MTB_API int32_t gpu_unregister_host(const double *ptr) {
     if (!ptr || it == R.regions.end()) {
         set_error("gpu_unregister_host: %p is not the start of a registered buffer", (const void *)ptr);
         return MTB_BAD_ARGS;
-    }
-    const HostRegion r = it->second;
-    if (r.hi > r.lo) {
-        // Every device of the session idle first: the runtime keeps a registration's GPU mapping (and the driver's
-        // userptr object behind it) alive while commands that used it are not retired, and only retires them at a
-        // synchronisation.  Unregistered but still mapped, the pages are freed by the caller and can come back at the
-        // same address as a later pageable copy's destination, which the runtime then pins over the stale mapping:
-        // the round-5 closing-suite fault (hipErrorIllegalAddress in Tensor.cpu(), reproduced by
-        // test_pageable_copies_after_registrations).  Registrations are long-lived; the wait is rare.
-        int cur = 0;
-        (void)hipGetDevice(&cur);  // the caller's current device is restored below
-        for (auto &d : S->devs) {
-            (void)hipSetDevice(d->dev);
-            if (hipDeviceSynchronize() != hipSuccess) {
-                (void)hipGetLastError();
-                (void)hipSetDevice(cur);
-                set_error("gpu_unregister_host: device %d did not synchronise; the buffer is still page-locked", d->dev);
-                return MTB_INTERNAL_ERROR;
-            }
-        }
-        (void)hipSetDevice(cur);
-        const hipError_t e = hipHostUnregister((void *)r.lo);
-        if (e != hipSuccess) {  // the range stays registered (and in the table): the caller must not free it
-            (void)hipGetLastError();
-            set_error("hipHostUnregister(%p): %s; the buffer is still page-locked", (void *)r.lo, hipGetErrorString(e));
-            return MTB_INTERNAL_ERROR;
-        }
-        R.regions.erase(it);
-        for (auto &d : S->devs) {  // and the unregistration itself retired before the caller may free the pages
-            (void)hipSetDevice(d->dev);
-            (void)hipDeviceSynchronize();
-        }
-        (void)hipSetDevice(cur);
-        if (hip_knows_host((const void *)r.lo) || hip_knows_host((const void *)(r.hi - 1))) {
-            set_error("gpu_unregister_host: HIP still maps [%p, %p) after hipHostUnregister", (void *)r.lo, (void *)r.hi);
-            return MTB_INTERNAL_ERROR;
-        }
-        return MTB_OK;
     }
     R.regions.erase(it);
     return MTB_OK;

@@ -195,8 +195,8 @@ def spectrum_batch(series: np.ndarray, window_len: int, hop: int, detrend="none"
                    trend_period: int = 0, precision="f64", output="power", max_records: int | None = None,
                    out: np.ndarray | None = None) -> np.ndarray:
     """gpu_spectrum_batch over a chronological series -> (nwin, record) array.  `out`: a
-    caller-owned C-contiguous float64 array of at least nwin * record elements (e.g. one
-    registered with register_host, which the library then fills by DMA directly)."""
+    caller-owned C-contiguous float64 array of at least nwin * record elements (the library
+    drains its pinned output ring into it)."""
     s = np.ascontiguousarray(series, dtype=np.float64)
     nwin = 1 + (s.size - window_len) // hop
     rec = _record(window_len, output)
@@ -269,22 +269,23 @@ def free_job(job_id: int) -> int:
 
 
 def register_host(a: np.ndarray) -> None:
-    """gpu_register_host: page-lock a C-contiguous float64 array for the session (FeedCache
-    history, output arrays); synchronous batch calls then DMA straight from / into it."""
+    """gpu_register_host: record a C-contiguous float64 array (FeedCache history, output arrays) for the
+    session.  Round 6: nothing is page-locked -- calls stage through the library's own pinned buffers
+    (DESIGN.md 4.2); overlapping registrations are refused."""
     if a.dtype != np.float64 or not a.flags.c_contiguous:
         raise ValueError("register_host needs a C-contiguous float64 array")
     _check("gpu_register_host", lib().gpu_register_host(_dptr(a), a.size))
 
 
 def unregister_host(a: np.ndarray) -> None:
-    """gpu_unregister_host: raises on every failure -- an unknown buffer (BAD_ARGS) and a runtime that
-    refused or still maps the range (INTERNAL_ERROR: the buffer stays page-locked and must not be freed)."""
+    """gpu_unregister_host: raises on every failure (an unknown buffer: BAD_ARGS; no session:
+    BACKEND_UNAVAILABLE)."""
     _check("gpu_unregister_host", lib().gpu_unregister_host(_dptr(a)))
 
 
 def set_host_locking(mode: int) -> int:
-    """gpu_set_host_locking: 1 = register_host page-locks the whole pages inside a buffer, 0 = it only records
-    the range (the default; calls stage).  Returns the previous mode."""
+    """gpu_set_host_locking: 0 (record the range, calls stage) is the only mode and returns 0; 1 (page-lock
+    caller memory, opt-in in round 5) was withdrawn in round 6 and raises BAD_ARGS."""
     r = int(lib().gpu_set_host_locking(mode))
     if r < 0:
         _check("gpu_set_host_locking", r)

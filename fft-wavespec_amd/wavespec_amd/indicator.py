@@ -5,8 +5,9 @@ Same names, argument meaning and error behaviour as the MQL5 code that calls
 
 * :class:`FeedCache` / :func:`ensure_feed_cache` -- Include/FeedCache.mqh:20-115
   (file format: int32 count + doubles, newest first); :func:`pin_feed_cache`
-  keeps the history page-locked (gpu_register_host) so the batch path DMAs it
-  in place -- the north star's "FeedCache rewired to pinned buffers".
+  registers the history with the session (gpu_register_host) across growth; the
+  batch path stages it through the library's pinned buffers for hipMemcpyAsync
+  -- the north star's "FeedCache rewired to pinned buffers".
 * :class:`FeedBuilder` -- FeedBuilder::Build / BuildPlaPriceSeries (1.1.0:474-506, 760-771).
 * :class:`FftProcessor` -- EnsureGpu + FftProcessor::Run (1.1.0:511-533, 722-757).
 * :func:`on_calculate` -- the per-bar OnCalculate loop restricted to the
@@ -129,10 +130,10 @@ def _restage(cache: FeedCache) -> None:
 
 
 def pin_feed_cache(cache: FeedCache) -> None:
-    """Page-lock the feed history for the device (gpu_register_host, needs an open session):
-    synchronous batch calls on ``cache.chrono`` then DMA it in place instead of copying it
-    through the library's staging buffers (include/mtbridge.h, "Pinned feed staging").  The
-    session that holds the registration is remembered (gpu_session_id)."""
+    """Register the feed history with the session (gpu_register_host, needs an open session); batch
+    calls on ``cache.chrono`` stage it through the library's pinned buffers (include/mtbridge.h,
+    "Pinned feed staging"; round 6: caller memory is never page-locked).  The session that holds
+    the registration is remembered (gpu_session_id)."""
     if cache.chrono.size != cache.close.size:
         cache.chrono = np.ascontiguousarray(cache.close[::-1], dtype=np.float64)
     if cache.chrono.size and not cache.pinned:
@@ -144,9 +145,8 @@ def pin_feed_cache(cache: FeedCache) -> None:
 def unpin_feed_cache(cache: FeedCache) -> None:
     """gpu_unregister_host of the pinned history.  A registration belongs to the session that made it:
     once the last gpu_shutdown has torn that session down (FftProcessor.shutdown in on_calculate may be
-    that call) the pages were unlocked with it, so there is nothing to undo -- the session id tells.
-    Under the same session every failure is raised: an unregistration that did not happen leaves the
-    buffer page-locked, and freeing it then is what the round-4 faults were made of."""
+    that call) its registrations went with it, so there is nothing to undo -- the session id tells.
+    Under the same session every failure is raised."""
     if not cache.pinned:
         return
     if bridge.session_id() != cache.pinned_session:

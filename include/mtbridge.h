@@ -228,45 +228,33 @@ MTB_API int32_t gpu_spectrum_topk_phase_batch(const double *series, int32_t seri
 MTB_API int32_t gpu_set_kalman_params(const double *params, int32_t n);
 
 /* Pinned feed staging (north star: "FeedCache.mqh rewired to stage price bars
- * into pinned host buffers for hipMemcpyAsync").  Replaces the FeedCache
- * close-history array's plain host memory (Include/FeedCache.mqh:36-115,
- * `struct FeedCache`) as the staging area: the caller page-locks the array it
- * already keeps (hipHostRegister, portable across the session's devices) after
- * each ArrayResize, and the synchronous batch calls (gpu_spectrum_batch, the
- * top-k variants, gpu_fft_real_forward_batch) then DMA an fp64 series straight
- * from it and write a whole fp64 result straight into a registered output
- * array -- no copy through the library's own staging buffers.  fp32 plans
- * convert and truncated outputs (out_cap below all records) still stage;
- * gpu_submit_spectrum_batch still copies its input (1.1.0:1316).
- * Registrations belong to the session and end with it (last gpu_shutdown).
+ * into pinned host buffers for hipMemcpyAsync"; replaces the plain-host-memory
+ * use of the FeedCache close history, Include/FeedCache.mqh:36-115,
+ * `struct FeedCache`).  Every batch call stages the caller's series through
+ * the library's own pinned (hipHostMalloc) buffers, chunk by chunk, while
+ * earlier chunks' H2D copies and kernels run; a synchronous call's records come
+ * back through a ring of four pinned slots that the host drains into the
+ * caller's array while the next chunks are copied off the device (so an
+ * output-dominated call overlaps its host copy-out with PCIe).
  *
- * Page granularity (round 5; page-locking is opt-in, gpu_set_host_locking):
- * only the whole pages INSIDE [ptr, ptr + count) are page-locked -- the page-exact span [round_up(ptr, 4096),
- * round_down(ptr + count, 4096)) -- never a page the buffer shares with other
- * memory; the < 1-page head and tail of the buffer go through a small pinned
- * bounce buffer of each call.  A buffer with no whole page inside is
- * registered without locking anything (its calls stage).  After
- * hipHostRegister / hipHostUnregister the library checks with
- * hipPointerGetAttributes that the runtime maps / no longer maps the span.
- *
- * The caller must not free, move (ArrayResize) or unregister a buffer while
- * it is registered and a call reading it runs, and must unregister it before
- * freeing it.  MTB_OK; MTB_BAD_ARGS for null/empty ranges, ranges overlapping
- * another registration or already page-locked memory (register) or an unknown
- * base pointer (unregister); MTB_BACKEND_UNAVAILABLE without a session;
- * MTB_INTERNAL_ERROR when the runtime refuses, or when after unregistering it
- * still maps the span -- a failed hipHostUnregister leaves the registration in
- * place (the buffer stays locked and must not be freed). */
+ * gpu_register_host records [ptr, ptr + count) with the session: it refuses
+ * ranges overlapping another registration, and registrations end with the
+ * session (last gpu_shutdown).  It does NOT page-lock the caller's memory
+ * (round 6): hipHostRegister of caller arrays was withdrawn because, after a
+ * locked array was unregistered and freed, a later pageable copy into memory
+ * reused from its pages could fault inside the HIP runtime.
+ * No call of this library page-locks, maps or DMAs caller memory, so freeing,
+ * moving (ArrayResize) or unregistering a buffer has no device-side hazard; a
+ * buffer must still not be freed while a call reading it runs.
+ * MTB_OK; MTB_BAD_ARGS for null/empty ranges, ranges overlapping another
+ * registration (register) or an unknown base pointer (unregister);
+ * MTB_BACKEND_UNAVAILABLE without a session. */
 MTB_API int32_t gpu_register_host(const double *ptr, int64_t count);
 MTB_API int32_t gpu_unregister_host(const double *ptr);
-/* Whether gpu_register_host page-locks (mode 1) or only records the range
- * (mode 0, the default: calls on a registered buffer stage through the
- * library's pinned buffers -- the same results; the host path is PCIe-bound
- * either way).  Round 5: with page-locking, a process that registers,
- * unregisters and frees a buffer can later fault (hipErrorIllegalAddress) in a
- * pageable copy into memory reused from those pages, ROCm 7.x.
- * Affects later registrations only.  Returns the previous mode, or MTB_BAD_ARGS
- * for a mode other than 0 / 1. */
+/* Round 5 made page-locking of registered caller memory opt-in (mode 1);
+ * round 6 withdrew it.  Mode 0 (record the range, stage through
+ * the library's pinned buffers) is the only mode: 0 returns 0, 1 returns
+ * MTB_BAD_ARGS with a last-error text saying so, any other mode MTB_BAD_ARGS. */
 MTB_API int32_t gpu_set_host_locking(int32_t mode);
 /* The current session's identity: a number > 0 that changes whenever the
  * session is torn down (last gpu_shutdown) and a new one opened; 0 without a
@@ -369,8 +357,10 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    two-pass row kernel in plain block order (the default is XCD-aware);
  *    8 = two passes with 8-column column-pass workgroups at M2 = 256 (fp64
  *    N = 65536 / 131072);
- *  - fp32 Kalman pre-pass: 1 = single-wave workgroups only, 2 = the sequential
- *    one-lane-per-window filter;
+ *  - fp32 Kalman pre-pass (spectrum plans, N <= 16384): 1 = single-wave
+ *    workgroups of the one-lane filter, 2 = the sequential one-lane filter,
+ *    7 = the packed two-segment filter with its rows written through to memory
+ *    (bit-identical to 0);
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
  *    with the AoS exchange; 3 = 0 with the element loads in natural order

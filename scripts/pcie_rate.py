@@ -2,8 +2,10 @@
 point gpu_spectrum_batch (pinned staging + H2D + kernel + D2H + copy-out),
 for DESIGN.md sec. 5 -- never bench.py's `value`.
   python3 scripts/pcie_rate.py [config] [--registered] [--topk]
---registered: the series and the output array are registered first
-(gpu_register_host, the pinned FeedCache): DMA in place, no staging copies.
+--registered: the series and the output array are registered first (gpu_register_host, the pinned
+FeedCache).  Round 6: registration records the range only; both forms stage the series through pinned
+buffers and return the records through the library's pinned output ring (rounds 2-5 DMA'd registered
+arrays in place, a mode withdrawn in round 6).
 --topk: gpu_spectrum_topk_batch (top-8 records in periods [18, 200]) instead of the N/2 powers:
 the D2H the fused scan removes ("the PCIe wall of C4/C5")."""
 import json
@@ -47,5 +49,5 @@ bytes_moved = (s.size + out.size) * 8
 print(json.dumps({"config": cfg, "seconds": ts, "windows_per_s": w / best,
                   "host_bytes_per_s": bytes_moved / best, "registered": registered, "output": "topk8" if topk else "power",
                   "register_seconds": t_reg if registered else None,
-                  "note": "gpu_spectrum_batch from host memory, 1 GPU" + (
-                      " (series and output registered: DMA in place)" if registered else " (staged)")}))
+                  "note": "gpu_spectrum_batch from host memory, 1 GPU, pinned staging + pinned output ring" + (
+                      " (series and output registered: recorded only)" if registered else "")}))

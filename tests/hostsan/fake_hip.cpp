@@ -111,29 +111,15 @@ int dev_of(const void *p) {  // -1: not device memory (host, pinned or registere
     --it;
     return a < it->first + it->second.first ? it->second.second : -1;
 }
-// page-locked host ranges: base -> bytes (hipHostRegister)
-std::mutex g_reg_mu;
-std::map<uintptr_t, size_t> g_regs;
-// Streams whose direct copies used a registration since the last device-wide synchronisation: the real runtime
-// kept a registration's mapping alive past hipHostUnregister while the commands that used it were not retired, and
-// the library's own stream synchronisation did not retire them -- a device synchronisation did (the round-5
-// closing-suite fault and its fix) -- so here only hipDeviceSynchronize retires them, and
-// unregistering while any remain counts as a violation.
-std::map<uintptr_t, std::set<ihipStream_t *>> g_reg_users;
+// Round 6: the library never page-locks caller memory (gpu_set_host_locking(1) withdrawn) and
+// every host <-> device copy it makes goes through its own pinned (hipHostMalloc) buffers.  Any hipHostRegister /
+// hipHostUnregister call counts as a violation, and a copy whose host side is not hipHostMalloc'd memory counts
+// as a direct copy of caller memory (fakehip_direct_copies, which the stress driver requires to stay 0).
 std::atomic<int64_t> g_direct{0};
-bool reg_covers(const void *p, size_t n) {
-    const uintptr_t a = (uintptr_t)p;
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.upper_bound(a);
-    if (it == g_regs.begin()) return false;
-    --it;
-    return a >= it->first && a + n <= it->first + it->second;
-}
 // hipHostMalloc'd blocks: base -> bytes
 std::mutex g_pinned_mu;
 std::map<uintptr_t, size_t> g_pinned;
 bool host_locked(const void *p) {
-    if (reg_covers(p, 1)) return true;
     const uintptr_t a = (uintptr_t)p;
     std::lock_guard<std::mutex> lk(g_pinned_mu);
     auto it = g_pinned.upper_bound(a);
@@ -206,48 +192,15 @@ hipError_t hipHostFree(void *p) {
     free(p);
     return hipSuccess;
 }
-// Page-locked host ranges (hipHostRegister).  The library must register whole pages only (round 5: the
-// page-exact span inside the caller's buffer): a range that is not page-aligned at both ends,
-// or that shares a page with a live registration, counts as a violation and is refused.  Copies whose host
-// side lies in a registered range count as direct (fakehip_direct_copies).
-hipError_t hipHostRegister(void *p, size_t n, unsigned int) {
-    const uintptr_t a = (uintptr_t)p;
-    if (!p || !n || a % 4096 || n % 4096) {
-        g_violations++;
-        return hipErrorInvalidValue;
-    }
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.lower_bound(a);
-    if ((it != g_regs.end() && it->first < a + n) || (it != g_regs.begin() && std::prev(it)->first + std::prev(it)->second > a)) {
-        g_violations++;
-        return hipErrorHostMemoryAlreadyRegistered;
-    }
-    g_regs[a] = n;
-    return hipSuccess;
+hipError_t hipHostRegister(void *, size_t, unsigned int) {
+    g_violations++;
+    return hipErrorInvalidValue;
 }
-hipError_t hipHostUnregister(void *p) {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.find((uintptr_t)p);
-    if (it == g_regs.end()) return hipErrorHostMemoryNotRegistered;
-    auto u = g_reg_users.find((uintptr_t)p);
-    if (u != g_reg_users.end() && !u->second.empty()) g_violations++;  // commands that used it not yet retired
-    g_reg_users.erase((uintptr_t)p);
-    g_regs.erase(it);
-    return hipSuccess;
+hipError_t hipHostUnregister(void *) {
+    g_violations++;
+    return hipErrorHostMemoryNotRegistered;
 }
-void note_reg_use(const void *host, size_t n, ihipStream_t *st) {
-    const uintptr_t a = (uintptr_t)host;
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.upper_bound(a);
-    if (it == g_regs.begin()) return;
-    --it;
-    if (a >= it->first && a + n <= it->first + it->second) g_reg_users[it->first].insert(st);
-}
-void retire_reg_uses() {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (auto &u : g_reg_users) u.second.clear();
-}
-// registered / pinned host memory: hipMemoryTypeHost; device memory: hipMemoryTypeDevice; anything else
+// pinned host memory: hipMemoryTypeHost; device memory: hipMemoryTypeDevice; anything else
 // (pageable memory) an error, as the real runtime answers (scripts/hostreg_probe.py)
 hipError_t hipPointerGetAttributes(hipPointerAttribute_t *attr, const void *p) {
     memset(attr, 0, sizeof(*attr));
@@ -282,10 +235,7 @@ hipError_t hipMemset(void *d, int v, size_t n) {
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st) {
     check_op(st, {d, s});
     const void *host = k == hipMemcpyHostToDevice ? s : (k == hipMemcpyDeviceToHost ? d : nullptr);
-    if (host && reg_covers(host, n)) {
-        g_direct++;
-        note_reg_use(host, n, st);
-    }
+    if (host && (!host_locked(host) || !host_locked((const char *)host + n - 1))) g_direct++;
     run_on(st, [=] { memcpy(d, s, n); });
     return hipSuccess;
 }
@@ -318,7 +268,6 @@ hipError_t hipDeviceSynchronize(void) {
         std::lock_guard<std::mutex> lk(g_streams_mu);
         for (auto *s : g_streams) s->drain();
     }
-    retire_reg_uses();
     return hipSuccess;
 }
 hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned int) {
@@ -375,10 +324,7 @@ void fakehip_reset(void) {
 int64_t fakehip_windows(int dev) { return dev >= 0 && dev < kMaxDev ? g_windows[dev].load() : -1; }
 int64_t fakehip_violations(void) { return g_violations.load(); }
 int64_t fakehip_direct_copies(void) { return g_direct.load(); }
-int64_t fakehip_registered_ranges(void) {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    return (int64_t)g_regs.size();
-}
+int64_t fakehip_registered_ranges(void) { return 0; }  // nothing is ever page-locked (round 6)
 }  // extern "C"
 
 // ---- kernel launch stubs (wsp_internal.h): record element k of window w = x_w[k % N] + k

@@ -228,9 +228,10 @@ void pinned_feed(int sym) {  // FeedCache rewired to pinned buffers, one chart's
     A.shutdown();
 }
 
-// registered ranges that do not start or end on a page: the library locks only the whole pages inside them
-// (the fake runtime refuses anything else and counts it as a violation), DMAs those in place and routes the
-// head / tail through its bounce buffer -- every record must still land, and the in-place copies must happen
+// registered ranges that do not start or end on a page (round 6: registration only records the range): every
+// record must land, no copy may touch the caller's memory directly (the fake runtime counts host sides that are
+// not hipHostMalloc'd), and the batch goes through the library's pinned output ring (the sanitizer builds cut
+// parts at 64 KiB, WSP_PART_BYTES, so these outputs wrap the 4-slot ring many times)
 int64_t (*g_direct_copies)(void) = nullptr;
 int64_t (*g_violations)(void) = nullptr;
 int64_t (*g_registered)(void) = nullptr;
@@ -252,7 +253,14 @@ void pinned_edges(int sym) {
         CHECK(A.batch(s, len, n, hop, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, out,
                       nwin * rec, &got) == MTB_OK && got == nwin, "edges batch %d", sym);
         CHECK(check_records(s0, out, n, hop, nwin, rec), "edges records %d round %d", sym, r);
-        CHECK(g_direct_copies() > d0, "edges: no in-place DMA %d", sym);
+        CHECK(g_direct_copies() == d0, "edges: a copy touched caller memory directly %d", sym);
+        // a truncated output (out_cap inside a part): exactly the records below the cap, nothing past it
+        const int cap_rec = nwin / 3 + 1;
+        std::fill(out, out + (size_t)nwin * rec, -7.0);
+        CHECK(A.batch(s, len, n, hop, MTB_DETREND_NONE, MTB_WINDOW_HANN, 0, MTB_PREC_F64, MTB_OUT_POWER, out,
+                      cap_rec * rec + rec / 2, &got) == MTB_OK && got == cap_rec, "edges truncated batch %d", sym);
+        CHECK(check_records(s0, out, n, hop, cap_rec, rec), "edges truncated records %d", sym);
+        CHECK(out[(size_t)cap_rec * rec] == -7.0 && out[(size_t)nwin * rec - 1] == -7.0, "edges: past out_cap %d", sym);
         CHECK(A.unreg(out) == MTB_OK && A.unreg(s) == MTB_OK, "unregister edges %d", sym);
     }
     // a buffer with no whole page inside: registered (nothing locked), its batches stage
@@ -305,10 +313,10 @@ int main(int argc, char **argv) {
     sym(h, A.plan_destroy, "wsp_plan_destroy");
     sym(h, A.reg, "gpu_register_host");
     sym(h, A.unreg, "gpu_unregister_host");
-    {  // the page-locking form (opt-in since round 5): the fake runtime checks its page-exact spans
+    {  // page-locking caller memory: opt-in in round 5, withdrawn in round 6 (mode 1 refused, 0 the only mode)
         decltype(&gpu_set_host_locking) lock_mode = nullptr;
         sym(h, lock_mode, "gpu_set_host_locking");
-        CHECK(lock_mode(1) == 0, "host locking was off by default");
+        CHECK(lock_mode(1) == MTB_BAD_ARGS && lock_mode(0) == 0 && lock_mode(2) == MTB_BAD_ARGS, "host locking mode");
     }
     sym(h, A.group_create, "wsp_group_create");
     sym(h, A.group_execute, "wsp_group_execute");

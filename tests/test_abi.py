@@ -113,17 +113,20 @@ def test_unknown_job_and_plan():
 
 
 def test_host_locking_mode():
-    """gpu_set_host_locking: record-only (0) by default, returns the previous mode, refuses anything but 0 / 1
-    (no session needed: it only selects what later registrations do)."""
+    """gpu_set_host_locking: round 6 withdrew page-locking of caller memory -- 0 (record the range,
+    stage through the library's pinned buffers) is the only mode and returns 0, 1 is refused with an explanation,
+    anything else is refused (no session needed)."""
     L = bridge.lib()
     assert L.gpu_set_host_locking(2) == bridge.BAD_ARGS
     assert L.gpu_set_host_locking(-1) == bridge.BAD_ARGS
-    assert bridge.set_host_locking(1) == 0
-    assert bridge.set_host_locking(1) == 1
-    assert bridge.set_host_locking(0) == 1
+    assert L.gpu_set_host_locking(1) == bridge.BAD_ARGS
+    assert "withdrawn" in bridge.last_error()
     assert bridge.set_host_locking(0) == 0
-    with pytest.raises(bridge.BridgeError):
-        bridge.set_host_locking(7)
+    assert bridge.set_host_locking(0) == 0
+    for mode in (1, 7):
+        with pytest.raises(bridge.BridgeError) as e:
+            bridge.set_host_locking(mode)
+        assert e.value.status == bridge.BAD_ARGS
 
 
 @pytest.mark.skipif(GPU, reason="checks the no-GPU behaviour")
