@@ -22,7 +22,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -762,6 +764,7 @@ struct Batch {
     void *h_in = nullptr, *h_out = nullptr;  // pinned staging (h_out: async jobs; synchronous calls use the ring)
     size_t h_in_bytes = 0, h_out_bytes = 0;
     std::vector<void *> ring;                // synchronous calls: pinned output slots, part i -> ring[i % size]
+    std::map<int64_t, int64_t> staged;       // series element ranges [first, second) already in h_in
     size_t ring_bytes = 0;
     int status = MTB_OK;
     std::string error;
@@ -781,8 +784,41 @@ struct Batch {
     }
 };
 
-// Host-side copies of large batches on several threads (one memcpy thread
-// reaches ~10 GB/s, well below PCIe): f(begin, end) over [0, n) in slices.
+// Host-side copies of large batches on several threads (one memcpy thread reaches ~10 GB/s, well below PCIe):
+// f(begin, end) over [0, n) in slices of at least min_per_thread, on up to 8 threads -- the caller's and the
+// copy pool's.  The pool's 7 workers are started once and live as long as the process (a synchronous batch of 64
+// parts makes two such calls per part: thread start-up per call would cost milliseconds).  Calls from many
+// threads at once (28 charts) share the workers; every caller runs its first slice itself, so each call progresses.
+struct CopyPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    int started = 0;
+    void submit(std::function<void()> f) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (started < 7) {
+            ++started;
+            std::thread([this] {
+                for (;;) {
+                    std::function<void()> t;
+                    {
+                        std::unique_lock<std::mutex> l(mu);
+                        cv.wait(l, [this] { return !q.empty(); });
+                        t = std::move(q.front());
+                        q.pop_front();
+                    }
+                    t();
+                }
+            }).detach();
+        }
+        q.push_back(std::move(f));
+        cv.notify_one();
+    }
+};
+CopyPool &copy_pool() {
+    static CopyPool *p = new CopyPool();  // intentionally leaked with its detached workers (process lifetime)
+    return *p;
+}
 template <typename F> void par_for(int64_t n, int64_t min_per_thread, F f) {
     const int64_t want = n / std::max<int64_t>(1, min_per_thread);
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(want, 8));
@@ -790,17 +826,32 @@ template <typename F> void par_for(int64_t n, int64_t min_per_thread, F f) {
         f(0, n);
         return;
     }
-    std::vector<std::thread> th;
+    struct Latch {
+        std::mutex m;
+        std::condition_variable cv;
+        int left = 0;
+    } L;
     const int64_t per = (n + nt - 1) / nt;
     for (int t = 1; t < nt; ++t) {
         const int64_t b0 = t * per, b1 = std::min<int64_t>(n, b0 + per);
-        if (b0 < b1) th.emplace_back([=] { f(b0, b1); });
+        if (b0 >= b1) continue;
+        {
+            std::lock_guard<std::mutex> lk(L.m);
+            ++L.left;
+        }
+        copy_pool().submit([&L, &f, b0, b1] {
+            f(b0, b1);
+            std::lock_guard<std::mutex> lk(L.m);  // notify under the lock: the waiter cannot return (and free L) first
+            if (--L.left == 0) L.cv.notify_one();
+        });
     }
     f(0, std::min<int64_t>(n, per));
-    for (auto &x : th) x.join();
+    std::unique_lock<std::mutex> lk(L.m);
+    L.cv.wait(lk, [&L] { return L.left == 0; });
 }
+constexpr int64_t kCopySlice = int64_t(1) << 19;  // elements per copy thread at least (4 MiB of fp64)
 void stage_in(void *dst, const double *src, int64_t n, bool f32) {  // series -> pinned staging
-    par_for(n, int64_t(4) << 20, [&](int64_t b0, int64_t b1) {
+    par_for(n, kCopySlice, [&](int64_t b0, int64_t b1) {
         if (f32) {
             float *d = static_cast<float *>(dst);
             for (int64_t i = b0; i < b1; ++i) d[i] = (float)src[i];
@@ -810,7 +861,7 @@ void stage_in(void *dst, const double *src, int64_t n, bool f32) {  // series ->
     });
 }
 void stage_out(double *dst, const void *src, int64_t n, bool f32) {  // pinned results -> caller
-    par_for(n, int64_t(4) << 20, [&](int64_t b0, int64_t b1) {
+    par_for(n, kCopySlice, [&](int64_t b0, int64_t b1) {
         if (f32) {
             const float *s = static_cast<const float *>(src);
             for (int64_t i = b0; i < b1; ++i) dst[i] = (double)s[i];
@@ -820,22 +871,21 @@ void stage_out(double *dst, const void *src, int64_t n, bool f32) {  // pinned r
     });
 }
 
-// Stages `series` (double, chronological) and enqueues every part.  A batch
-// is cut into parts: contiguous window ranges per device (the multi-GPU
-// shard), each cut again into chunks on the device's streams, so that the
-// host staging of chunk i+1, the H2D copy, the kernels and the D2H copy of
-// earlier chunks overlap.  Each part copies its own input slice (with the
-// N - hop halo of overlapping windows).
-// `ring` (synchronous calls): the parts are cut by input AND output bytes (>= 64 MiB each, up to 64 per
-// device) and their results are not copied off the device here: batch_ring_out moves them through a few
-// pinned slots, draining one into the caller's array while the next ones are in flight -- so an output-
-// dominated call (C4 from host memory: 8.4 MB in, 8 GiB out) overlaps its host copy-out with the PCIe
-// transfer and holds a few hundred MiB of pinned memory instead of the whole result.  Asynchronous jobs
-// (gpu_submit_spectrum_batch) keep the whole result in pinned staging until the caller polls.
+// A batch is cut into parts: contiguous window ranges per device (the multi-GPU shard), each cut again into
+// chunks on the device's streams, so that the host staging of chunk i+1, its H2D copy, the kernels and the D2H
+// copies of earlier chunks overlap.  Each part stages and copies its own input slice (with the N - hop halo of
+// overlapping windows).  Parts are ordered chunk-major across devices (chunk 0 of every device, then chunk 1,
+// ...), so that enqueueing and draining alternate between the devices.
+// `ring` (synchronous calls, run_sync): the parts are cut by input AND output bytes (>= WSP_PART_BYTES each, up to
+// 64 per device) and their records come back through a ring of kRingSlots pinned slots: the host drains one slot
+// into the caller's array while the D2H copies of the next parts are in flight, and stages the next parts' input
+// whenever no slot is ready -- so an output-dominated call (C4 from host memory: 8.4 MB in, 8 GiB out) overlaps
+// its copy-out with PCIe and holds a few hundred MiB of pinned memory instead of the whole result.  Asynchronous
+// jobs (gpu_submit_spectrum_batch) keep the whole result in pinned staging until the caller polls.
 #ifndef WSP_PART_BYTES
 #define WSP_PART_BYTES (64 << 20)  // the sanitizer builds (tests/hostsan) cut at 64 KiB to exercise many parts
 #endif
-int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out, bool ring = false) {
+int batch_plan(Session &S, const Config &c, std::unique_ptr<Batch> *out, bool ring) {
     auto b = std::make_unique<Batch>();
     b->cfg = c;
     {
@@ -843,8 +893,7 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
         memcpy(b->kalman, g_kalman, sizeof(g_kalman));
     }
     const size_t es = c.elem();
-    const int64_t in_elems = c.series_elems();
-    const size_t in_bytes = (size_t)in_elems * es, out_bytes = (size_t)(c.n_windows * c.record()) * es;
+    const size_t in_bytes = (size_t)c.series_elems() * es, out_bytes = (size_t)(c.n_windows * c.record()) * es;
     b->h_in_bytes = in_bytes;
     if (!(b->h_in = host_alloc(in_bytes))) return MTB_NO_MEM;
     if (!ring) {
@@ -859,11 +908,11 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
     const int64_t K = std::max<int64_t>(1, std::min<int64_t>({ring ? int64_t(64) : int64_t(16),
                                                               cut_bytes / (int64_t)WSP_PART_BYTES, per_dev}));
     const int64_t per = (per_dev + K - 1) / K;
-    int64_t staged = 0;  // series elements already in the pinned buffer
-    for (int g = 0; g < G; ++g) {
-        DeviceCtx &D = *S.devs[g];
-        const int64_t d0 = g * per_dev, d1 = std::min<int64_t>(c.n_windows, d0 + per_dev);
-        for (int64_t w0 = d0; w0 < d1; w0 += per) {
+    for (int64_t k = 0; k < K; ++k)
+        for (int g = 0; g < G; ++g) {
+            const int64_t d1 = std::min<int64_t>(c.n_windows, (g + 1) * per_dev), w0 = g * per_dev + k * per;
+            if (w0 >= d1) continue;
+            DeviceCtx &D = *S.devs[g];
             Part p;
             p.dev = D.dev;
             p.w0 = w0;
@@ -875,32 +924,62 @@ int batch_start(Session &S, const Config &c, const double *series, std::unique_p
             p.ws_bytes = ws_layout(pc, D.dev).total;
             p.stream = D.next_stream();
             b->parts.push_back(p);
-            Part &P = b->parts.back();
-            HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
-            P.d_in = dev_alloc(P.dev, P.in_bytes);
-            P.d_out = dev_alloc(P.dev, P.out_bytes);
-            if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
-            if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
-            P.done = event_alloc(P.dev);
-            if (!P.done) return MTB_INTERNAL_ERROR;
-            const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
-            if (e1 > staged) {  // stage the part's new samples while earlier parts' copies and kernels run
-                stage_in((char *)b->h_in + (size_t)staged * es, series + staged, e1 - staged, c.f32);
-                staged = e1;
-            }
-            HIP_OR(hipMemcpyAsync(P.d_in, (const char *)b->h_in + (size_t)e0 * es, P.in_bytes, hipMemcpyHostToDevice,
-                                  P.stream),
-                   MTB_INTERNAL_ERROR);
-            int st = enqueue(P.dev, pc, b->kalman, P.d_in, P.d_out, P.d_ws, P.stream);
-            if (st != MTB_OK) return st;
-            if (ring) continue;  // copied off the device by batch_ring_out
-            const size_t o0 = (size_t)(P.w0 * c.record()) * es;
-            HIP_OR(hipMemcpyAsync((char *)b->h_out + o0, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream),
-                   MTB_INTERNAL_ERROR);
-            HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
-            P.recorded = true;
         }
+    *out = std::move(b);
+    return MTB_OK;
+}
+
+// Stages part i's input slice, copies it to the device and enqueues its kernels (and, outside the ring, its D2H
+// copy into the pinned result buffer plus its completion event).
+int part_enqueue(Batch &b, int i, const double *series, bool ring) {
+    const Config &c = b.cfg;
+    const size_t es = c.elem();
+    Part &P = b.parts[i];
+    Config pc = c;
+    pc.n_windows = P.nw;
+    HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
+    P.d_in = dev_alloc(P.dev, P.in_bytes);
+    P.d_out = dev_alloc(P.dev, P.out_bytes);
+    if (P.ws_bytes) P.d_ws = dev_alloc(P.dev, P.ws_bytes);
+    if (!P.d_in || !P.d_out || (P.ws_bytes && !P.d_ws)) return MTB_NO_MEM;
+    P.done = event_alloc(P.dev);
+    if (!P.done) return MTB_INTERNAL_ERROR;
+    const int64_t e0 = P.w0 * c.hop, e1 = e0 + pc.series_elems();
+    // stage the samples of [e0, e1) no earlier part staged (the N - hop halo is shared with the neighbouring parts,
+    // whose H2D copies may still be reading it)
+    {
+        auto it = b.staged.upper_bound(e0);  // b.staged: disjoint, merged intervals
+        if (it != b.staged.begin() && std::prev(it)->second > e0) --it;
+        int64_t x = e0, lo = e0, hi = e1;
+        while (it != b.staged.end() && it->first <= e1) {  // overlapping or touching [e0, e1): merged below
+            if (it->first > x) stage_in((char *)b.h_in + (size_t)x * es, series + x, it->first - x, c.f32);
+            x = std::max(x, it->second);
+            lo = std::min(lo, it->first);
+            hi = std::max(hi, it->second);
+            it = b.staged.erase(it);
+        }
+        if (x < e1) stage_in((char *)b.h_in + (size_t)x * es, series + x, e1 - x, c.f32);
+        b.staged[lo] = hi;
     }
+    HIP_OR(hipMemcpyAsync(P.d_in, (const char *)b.h_in + (size_t)e0 * es, P.in_bytes, hipMemcpyHostToDevice, P.stream),
+           MTB_INTERNAL_ERROR);
+    int st = enqueue(P.dev, pc, b.kalman, P.d_in, P.d_out, P.d_ws, P.stream);
+    if (st != MTB_OK) return st;
+    if (ring) return MTB_OK;  // copied off the device by run_sync's ring
+    const size_t o0 = (size_t)(P.w0 * c.record()) * es;
+    HIP_OR(hipMemcpyAsync((char *)b.h_out + o0, P.d_out, P.out_bytes, hipMemcpyDeviceToHost, P.stream),
+           MTB_INTERNAL_ERROR);
+    HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+    P.recorded = true;
+    return MTB_OK;
+}
+
+// Asynchronous jobs: every part enqueued at once, results into pinned staging.
+int batch_start(Session &S, const Config &c, const double *series, std::unique_ptr<Batch> *out) {
+    std::unique_ptr<Batch> b;
+    int st = batch_plan(S, c, &b, false);
+    for (int i = 0; st == MTB_OK && i < (int)b->parts.size(); ++i) st = part_enqueue(*b, i, series, false);
+    if (st != MTB_OK) return st;
     *out = std::move(b);
     return MTB_OK;
 }
@@ -925,17 +1004,12 @@ int batch_poll(Batch &b, bool wait) {
     return MTB_OK;
 }
 
-// Copies finished records (converted to double) into the caller's buffer;
-// with `wait`, part by part as each one completes.
-int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int32_t *n_out) {
+// Copies the finished records (converted to double) of an asynchronous job into the caller's buffer.
+int batch_copy_out(const Batch &b, double *out, int64_t out_cap, int32_t *n_out) {
     const int64_t rec = b.cfg.record();
     const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
     for (const auto &p : b.parts) {
-        if (p.w0 >= nrec) break;
-        if (wait) {
-            const int st = part_poll(p, true);
-            if (st != MTB_OK) return st;
-        }
+        if (p.w0 >= nrec) continue;
         const int64_t r1 = std::min<int64_t>(p.w0 + p.nw, nrec);
         stage_out(out + p.w0 * rec, (const char *)b.h_out + (size_t)(p.w0 * rec) * b.cfg.elem(), (r1 - p.w0) * rec,
                   b.cfg.f32);
@@ -944,66 +1018,73 @@ int batch_copy_out(const Batch &b, double *out, int64_t out_cap, bool wait, int3
     return MTB_OK;
 }
 
-// Synchronous copy-out through the pinned ring (batch_start(ring = true)): the records of part i go device ->
-// ring[i % R] on the part's stream (after its kernel), and while the host drains slot i into the caller's array
-// the D2H copies of parts i+1 .. i+R-1 are in flight; slot i is refilled (part i+R) as soon as it is drained.
+// Synchronous batch: parts enqueued one by one, their records copied off the device into the pinned ring
+// (part outs[j] -> ring[j % R], on the part's stream after its kernels) and drained into the caller's array.
+// The host loop drains a slot as soon as its copy is complete, and otherwise stages and enqueues the next part;
+// with nothing left to enqueue it waits for the oldest slot.  Slot j is refilled (outs[j + R]) once drained.
 // Only the parts holding records below out_cap are copied.
 constexpr int kRingSlots = 4;
-int batch_ring_out(Batch &b, double *out, int64_t out_cap, int32_t *n_out) {
-    const int64_t rec = b.cfg.record();
-    const size_t es = b.cfg.elem();
-    const int64_t nrec = std::min<int64_t>(b.cfg.n_windows, out_cap / rec);
-    int np = 0;
-    size_t slot = 0;
-    for (const auto &p : b.parts) {
-        if (p.w0 >= nrec) break;
-        ++np;
-        slot = std::max(slot, p.out_bytes);
-    }
-    const int R = std::min(kRingSlots, np);
-    b.ring_bytes = slot;
-    for (int r = 0; r < R; ++r) {
-        b.ring.push_back(host_alloc(slot));
-        if (!b.ring.back()) return MTB_NO_MEM;
-    }
-    auto nrec_of = [&](const Part &p) { return std::min<int64_t>(p.w0 + p.nw, nrec) - p.w0; };
-    auto issue = [&](int i) -> int {
-        Part &P = b.parts[i];
-        HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
-        HIP_OR(hipMemcpyAsync(b.ring[i % R], P.d_out, (size_t)(nrec_of(P) * rec) * es, hipMemcpyDeviceToHost, P.stream),
-               MTB_INTERNAL_ERROR);
-        HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
-        P.recorded = true;
-        return MTB_OK;
-    };
-    for (int i = 0; i < R; ++i) {
-        const int st = issue(i);
-        if (st != MTB_OK) return st;
-    }
-    for (int i = 0; i < np; ++i) {
-        const Part &P = b.parts[i];
-        int st = part_poll(P, true);
-        if (st != MTB_OK) return st;
-        stage_out(out + P.w0 * rec, b.ring[i % R], nrec_of(P) * rec, b.cfg.f32);
-        if (i + R < np && (st = issue(i + R)) != MTB_OK) return st;
-    }
-    *n_out = (int32_t)nrec;
-    return MTB_OK;
-}
-
 int run_sync(const Config &c, const double *series, double *out, int64_t out_cap, int32_t *out_len) {
     auto S = session();
     if (!S) {
         set_error("gpu_init has not succeeded (no GPU session)");
         return MTB_BACKEND_UNAVAILABLE;
     }
-    std::unique_ptr<Batch> b;
-    int st = batch_start(*S, c, series, &b, true);
+    std::unique_ptr<Batch> bp;
+    int st = batch_plan(*S, c, &bp, true);
     if (st != MTB_OK) return st;
-    int32_t n = 0;
-    st = batch_ring_out(*b, out, out_cap, &n);
-    if (st != MTB_OK) return st;
-    if (out_len) *out_len = n;
+    Batch &b = *bp;
+    const int64_t rec = c.record();
+    const size_t es = c.elem();
+    const int64_t nrec = std::min<int64_t>(c.n_windows, out_cap / rec);
+    std::vector<int> outs;  // parts holding records below out_cap, in enqueue order
+    size_t slot = 0;
+    for (int i = 0; i < (int)b.parts.size(); ++i)
+        if (b.parts[i].w0 < nrec) {
+            outs.push_back(i);
+            slot = std::max(slot, b.parts[i].out_bytes);
+        }
+    const int R = std::min<int>(kRingSlots, (int)outs.size());
+    b.ring_bytes = slot;
+    for (int r = 0; r < R; ++r) {
+        b.ring.push_back(host_alloc(slot));
+        if (!b.ring.back()) return MTB_NO_MEM;
+    }
+    auto nrec_of = [&](const Part &p) { return std::min<int64_t>(p.w0 + p.nw, nrec) - p.w0; };
+    const int np = (int)b.parts.size(), no = (int)outs.size();
+    int enq = 0, issued = 0, drained = 0;
+    auto issue_ready = [&]() -> int {  // D2H copies of enqueued parts into free slots
+        while (issued < no && issued < drained + R && outs[issued] < enq) {
+            Part &P = b.parts[outs[issued]];
+            HIP_OR(hipSetDevice(P.dev), MTB_BACKEND_UNAVAILABLE);
+            HIP_OR(hipMemcpyAsync(b.ring[issued % R], P.d_out, (size_t)(nrec_of(P) * rec) * es, hipMemcpyDeviceToHost,
+                                  P.stream),
+                   MTB_INTERNAL_ERROR);
+            HIP_OR(hipEventRecord(P.done, P.stream), MTB_INTERNAL_ERROR);
+            P.recorded = true;
+            ++issued;
+        }
+        return MTB_OK;
+    };
+    while (drained < no || enq < np) {
+        if (drained < issued) {
+            const Part &P = b.parts[outs[drained]];
+            st = part_poll(P, enq >= np);  // block only when there is nothing left to stage
+            if (st == MTB_OK) {
+                stage_out(out + P.w0 * rec, b.ring[drained % R], nrec_of(P) * rec, c.f32);
+                ++drained;
+                if ((st = issue_ready()) != MTB_OK) return st;
+                continue;
+            }
+            if (st != MTB_NOT_READY) return st;
+        }
+        if (enq < np) {
+            if ((st = part_enqueue(b, enq, series, true)) != MTB_OK) return st;
+            ++enq;
+            if ((st = issue_ready()) != MTB_OK) return st;
+        }
+    }
+    if (out_len) *out_len = (int32_t)nrec;
     return MTB_OK;
 }
 
@@ -1756,7 +1837,7 @@ MTB_API int32_t gpu_try_get_spectrum_batch(int64_t job_id, double *out, int32_t 
         return MTB_BAD_ARGS;
     }
     int32_t n = 0;
-    const int cst = batch_copy_out(*b, out, out_cap, false, &n);
+    const int cst = batch_copy_out(*b, out, out_cap, &n);
     if (cst != MTB_OK) return cst;
     if (out_len) *out_len = n;
     return MTB_OK;
