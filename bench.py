@@ -68,6 +68,7 @@ def parse(argv=None):
                     help="hop = 1 top-k: segments per seed workgroup (wsp_plan_set_seed_chain; 0 = library policy)")
     ap.add_argument("--variant", type=int, default=0, help="kernel form (wsp_plan_set_variant; ablations)")
     ap.add_argument("--chunk", type=int, default=0, help="windows per chunk of the two-pass large-N path (wsp_plan_set_chunk)")
+    ap.add_argument("--grid", type=int, default=0, help="workgroups of the FFT-kernel / inverse launch (wsp_plan_set_grid)")
     ap.add_argument("--c5-layout", default="greedy", choices=["length", "greedy", "nlogn"],
                     help="C5: symbols to streams by window length, or greedy by output bytes / by N log N work")
     ap.add_argument("--c5-streams", type=int, default=0,
@@ -355,7 +356,7 @@ class SingleBatch(Workload):
     """One plan over one window batch (every config but C5)."""
 
     def __init__(self, name, rank, local_rank, world, scaling, algo="auto", slide_seg=0, variant=0, chunk=0,
-                 seed_chain=0):
+                 seed_chain=0, grid=0):
         import torch
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
@@ -378,6 +379,8 @@ class SingleBatch(Workload):
             self.plan = bridge.Plan.inverse(local_rank, n, nw)
             if variant:
                 self.plan.set_variant(variant)
+            if grid:
+                self.plan.set_grid(grid)
         else:
             full = synth.random_walk_torch((w - 1) * hop + n, seed, dev, tdt)  # resident in HBM
             self.series = full[a:b].contiguous() if (a, b) != (0, full.numel()) else full
@@ -395,6 +398,8 @@ class SingleBatch(Workload):
                 self.plan.set_seed_chain(seed_chain)
             if chunk:
                 self.plan.set_chunk(chunk)
+            if grid:
+                self.plan.set_grid(grid)
         self.algorithm = self.plan.algorithm() if output != "inverse" else "inverse"
         del full
         self.out = torch.empty(nw * self.plan.record, dtype=tdt, device=dev)
@@ -587,7 +592,7 @@ def main(argv=None):
                      args.c5_streams, args.c5_mode, args.c5_shard)
     else:
         wl = SingleBatch(args.config, shard_rank, local_rank, shard_world, scaling, args.algo, args.slide_seg,
-                         args.variant, args.chunk, args.seed_chain)
+                         args.variant, args.chunk, args.seed_chain, args.grid)
     torch.cuda.synchronize()
 
     settled = None if args.no_settle else settle(wl.step, wl.stream)

@@ -316,6 +316,7 @@ struct Config {
     int variant = 0;                    // kernel form (wsp_plan_set_variant: ablations), 0 = the library's choice
     unsigned char *scan_flags = nullptr;  // wsp_plan_set_scan_flags: per-window path of the probe-threshold top-k scan
     int64_t chunk = 0;                  // N > 16384 two-pass path: windows per chunk, 0 = large_chunk (wsp_plan_set_chunk)
+    int grid = 0;                       // workgroups of the FFT-kernel / inverse launch, 0 = the library's (wsp_plan_set_grid)
     int64_t chunk_windows() const;
     bool f32 = false;
     size_t elem() const { return f32 ? sizeof(float) : sizeof(double); }
@@ -546,6 +547,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         I.n_windows = c.n_windows;
         I.log2n = c.log2n;
         I.variant = c.variant;
+        I.grid = c.grid;
         HIP_OR(launch_inverse(I, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }
@@ -619,6 +621,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         return MTB_OK;
     }
     SpectrumLaunch L{};
+    L.grid = c.grid;
     L.series = d_series;
     L.hop = c.hop;
     L.detrend = c.detrend;
@@ -2121,6 +2124,17 @@ MTB_API int32_t wsp_plan_set_chunk(int64_t plan, int64_t windows) {
     const int sw = plan_ws_fit(*p);
     if (sw != MTB_OK) p->cfg = old;
     return sw;
+}
+
+MTB_API int32_t wsp_plan_set_grid(int64_t plan, int32_t workgroups) {
+    std::shared_ptr<Plan> p = find_plan(plan);
+    if (!p || workgroups < 0 || workgroups > 65536) {
+        set_error("wsp_plan_set_grid(%lld, %d): unknown plan or workgroups outside 0..65536", (long long)plan, workgroups);
+        return MTB_BAD_ARGS;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->cfg.grid = workgroups;
+    return MTB_OK;
 }
 
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan) {

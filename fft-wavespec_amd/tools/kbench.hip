@@ -57,6 +57,73 @@ __global__ __launch_bounds__(256) void copy11x4(const double2 *__restrict__ in, 
     }
 }
 
+// 1:1 copy, 4 x 16 B in flight per thread, non-temporal loads and stores (the inverse's store form)
+template <bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy11nt(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += 4 * stride) {
+        d2v v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = j + u * stride;
+            if (k < n) v[u] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const d2v *>(in + k))
+                                  : *reinterpret_cast<const d2v *>(in + k);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = j + u * stride;
+            if (k < n) {
+                if (NTS) __builtin_nontemporal_store(v[u], reinterpret_cast<d2v *>(out + k));
+                else *reinterpret_cast<d2v *>(out + k) = v[u];
+            }
+        }
+    }
+}
+
+// kbench copy [reps=20] [rounds=3]: the inverse's traffic as a pure 1:1 stream -- 65536 x 4096 fp64 read (2.147 GB)
+// and the same written, 16-B accesses, grid sweep; whole-GPU grids are multiples of 256 CUs.
+int copy_main(int reps, int rounds) {
+    const int64_t n2 = (int64_t)65536 * 4096 / 2;  // double2 elements
+    double2 *in, *out;
+    CK(hipMalloc(&in, n2 * 16));
+    CK(hipMalloc(&out, n2 * 16));
+    hipLaunchKernelGGL(fill_walk, dim3(4096), dim3(256), 0, 0, (double *)in, n2 * 2);
+    CK(hipMemset(out, 0, n2 * 16));
+    CK(hipDeviceSynchronize());
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = (double)n2 * 32;
+    printf("# 1:1 copy of %.3f GB read + %.3f GB written (the inverse plan's 65536 x 4096 fp64 in and out)\n", bytes / 2e9,
+           bytes / 2e9);
+    const char *nm[] = {"copy11", "copy11x4", "copy11-ntl", "copy11-nts", "copy11-nt2"};
+    for (int round = 0; round < rounds; ++round)
+        for (int kind = 0; kind < 5; ++kind)
+            for (int g : {1024, 2048, 4096, 8192, 16384, 32768}) {
+                auto go = [&] {
+                    if (kind == 0) hipLaunchKernelGGL(copy11, dim3(g), dim3(256), 0, s, in, out, n2);
+                    else if (kind == 1) hipLaunchKernelGGL((copy11nt<false, false>), dim3(g), dim3(256), 0, s, in, out, n2);
+                    else if (kind == 2) hipLaunchKernelGGL((copy11nt<true, false>), dim3(g), dim3(256), 0, s, in, out, n2);
+                    else if (kind == 3) hipLaunchKernelGGL((copy11nt<false, true>), dim3(g), dim3(256), 0, s, in, out, n2);
+                    else hipLaunchKernelGGL((copy11nt<true, true>), dim3(g), dim3(256), 0, s, in, out, n2);
+                };
+                go();
+                CK(hipEventRecord(e0, s));
+                for (int i = 0; i < reps; ++i) go();
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = ms * 1000.0 / reps;
+                printf("round %d %-11s grid=%6d  %8.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", round, nm[kind], g, us,
+                       bytes / us / 1e3, bytes / us / 1e3 / 8000.0);
+                fflush(stdout);
+            }
+    return 0;
+}
+
 // 2:1 with 4 independent loads in flight per thread, optional nt stores
 template <bool NT>
 __global__ __launch_bounds__(256) void copy21u(const double2 *__restrict__ in, double2 *__restrict__ out, int64_t n_out) {
@@ -311,6 +378,7 @@ int main(int argc, char **argv) {
         }
     }
     if (argc > 1 && std::string(argv[1]) == "out") return out_main(argc > 2 ? atoi(argv[2]) : 20);
+    if (argc > 1 && std::string(argv[1]) == "copy") return copy_main(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atoi(argv[3]) : 3);
     if (argc > 1 && std::string(argv[1]) == "store") {  // kbench store [reps=20] [rounds=4]: NT vs plain power-row stores
         const int reps = argc > 2 ? atoi(argv[2]) : 20, rounds = argc > 3 ? atoi(argv[3]) : 4;
         const int64_t W = 65536;

@@ -74,6 +74,7 @@ SIGNATURES = {
     "wsp_plan_set_variant": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_set_scan_flags": (C.c_int32, [C.c_int64, C.c_void_p]),
     "wsp_plan_set_chunk": (C.c_int32, [C.c_int64, C.c_int64]),
+    "wsp_plan_set_grid": (C.c_int32, [C.c_int64, C.c_int32]),
     "wsp_plan_create": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32]),
     "wsp_plan_create_inverse": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
@@ -358,6 +359,10 @@ class Plan:
     def set_chunk(self, windows: int) -> None:
         """Tuning: windows per chunk of the two-pass large-N path (0 = the library's ~192 MiB of column results)."""
         _check("wsp_plan_set_chunk", lib().wsp_plan_set_chunk(self.handle, windows))
+
+    def set_grid(self, workgroups: int) -> None:
+        """Tuning: workgroups of the FFT-kernel / inverse launch (0 = the library's 32768)."""
+        _check("wsp_plan_set_grid", lib().wsp_plan_set_grid(self.handle, workgroups))
 
     def set_scan_flags(self, d_flags: int) -> None:
         """Diagnostics: device buffer of n_windows bytes receiving each window's top-k scan path

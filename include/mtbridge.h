@@ -385,6 +385,12 @@ MTB_API int32_t wsp_plan_set_scan_flags(int64_t plan, void *d_flags);
  * 0 = the library's ~192 MiB of column results; grows the plan workspace as
  * needed.  MTB_BAD_ARGS for an unknown plan or windows outside 0..2^20. */
 MTB_API int32_t wsp_plan_set_chunk(int64_t plan, int64_t windows);
+/* Tuning: workgroups of the per-window FFT kernel's launch (grid-stride over
+ * window groups) and of the inverse plans' launch; 0 = the library's choice
+ * (32768).  Applies to the FFT-kernel and inverse paths only (the sliding DFT,
+ * Kalman pre-pass and large-N kernels size their own grids).  MTB_BAD_ARGS for
+ * an unknown plan or workgroups outside 0..65536. */
+MTB_API int32_t wsp_plan_set_grid(int64_t plan, int32_t workgroups);
 /* MTB_ALGO_FFT or MTB_ALGO_SLIDE: what the next execute runs. */
 MTB_API int32_t wsp_plan_get_algorithm(int64_t plan);
 
