@@ -717,38 +717,77 @@ __device__ __noinline__ double atan2_call(double y, double x) { return atan2(y, 
 // equals phi_i + 2 pi K_i with K_i the running count of +-1 corrections: K is
 // an exact integer prefix scan and u is one fma, so only the rounding of the
 // reference's running sum (not its decisions) differs.
-template <int LOG2N, int CH = 16, bool kCall = false>
+// Lane l <- lane l - 1 (wave_shr:1) / lane l + 1 (wave_shl:1) across the whole wave, one 64-bit value as two DPP
+// moves (gfx9 DPP; the lanes at the wave's ends read 0, and their callers do not use it).  tools/dpp_probe.hip
+// checks the direction on the device.
+__device__ __forceinline__ double dpp_from_prev_lane(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double dpp_from_next_lane(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), 0x130, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <int LOG2N, int CH = 16, bool kCall = false, bool kDpp = false>
 __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, double *scanbuf, double (&pw)[CH],
                                             double (&u)[CH], double (&gd)[CH]) {
     // CH = bins per thread (16: the whole row; smaller for the top-k records, which only need the
     // bins up to the scan range: CH * TPW >= kmax + 2, chosen at run time by the caller)
+    // kDpp (round 6, the full phase record): the two neighbour bins' phases are not recomputed -- they are the
+    // adjacent lanes' own first / last phases, moved by DPP (16 atan2 per lane instead of 18).  Where the neighbour
+    // lies in another wave of the window (N >= 4096: lane 0 of waves 1.., lane 63 of all but the last) the value
+    // comes through LDS at the unwrap scan's barrier, and that wave boundary's correction is added to the counts
+    // there.  The same atan2 values as recomputing them: bit-identical output.
     using G = Geo<LOG2N>;
     constexpr int M = G::M, TPW = G::TPW;
     constexpr double kPi = 3.14159265358979323846;  // M_PI
     constexpr double k2Pi = 2.0 * kPi;              // the reference's 2.0 * M_PI correction
     const int k0 = CH * t;
+    constexpr int SW = TPW < 64 ? TPW : 64;
+    const int lt = t & (SW - 1);
     double ph[CH + 2];  // bins k0 - 1 .. k0 + CH
+    if constexpr (kDpp) {
+        static_assert(CH == 16 && !kCall, "the DPP exchange serves the full phase record");
 #pragma unroll
-    for (int j = 0; j < CH + 2; ++j) {
-        const int k = k0 - 1 + j;
-        ph[j] = 0.0;  // bin M: the zeroed upper half, atan2(0, 0) = 0
-        if (k >= 0 && k < M) {
-            const cpx<double> x = xrow[pad16(k)];
-            ph[j] = kCall ? atan2_call(x.im, x.re) : atan2(x.im, x.re);
-            if (j >= 1 && j <= CH) pw[j - 1] = x.re * x.re + x.im * x.im;
+        for (int j = 1; j <= CH; ++j) {  // the thread's own bins, all < M
+            const cpx<double> x = xrow[pad16(k0 - 1 + j)];
+            ph[j] = atan2(x.im, x.re);
+            pw[j - 1] = x.re * x.re + x.im * x.im;
+        }
+        const double prv = dpp_from_prev_lane(ph[CH]), nxt = dpp_from_next_lane(ph[1]);
+        ph[0] = k0 == 0 ? 0.0 : prv;            // bin -1 does not exist (its correction is forced to 0)
+        ph[CH + 1] = k0 + CH >= M ? 0.0 : nxt;  // bin M: the zeroed upper half, atan2(0, 0) = 0
+    } else {
+#pragma unroll
+        for (int j = 0; j < CH + 2; ++j) {
+            const int k = k0 - 1 + j;
+            ph[j] = 0.0;  // bin M: the zeroed upper half, atan2(0, 0) = 0
+            if (k >= 0 && k < M) {
+                const cpx<double> x = xrow[pad16(k)];
+                ph[j] = kCall ? atan2_call(x.im, x.re) : atan2(x.im, x.re);
+                if (j >= 1 && j <= CH) pw[j - 1] = x.re * x.re + x.im * x.im;
+            }
         }
     }
+    // kDpp, several waves per window: lane 0 of waves 1.. and lane 63 of all waves but the last hold a neighbour
+    // from another wave, fixed after the barrier below
+    const bool wlead = kDpp && TPW >= 128 && lt == 0 && t > 0;
+    const bool wtail = kDpp && TPW >= 128 && lt == 63 && k0 + CH < M;
     int cj[CH + 1];  // correction count of bins k0 .. k0 + CH (UnwrapPhase :1068-1077)
 #pragma unroll
     for (int j = 0; j < CH + 1; ++j) {
         const double diff = ph[j + 1] - ph[j];
         cj[j] = (k0 + j == 0) ? 0 : diff > kPi ? -1 : diff < -kPi ? 1 : 0;
     }
+    if (wlead) cj[0] = 0;  // the wave boundary's correction: added below
     int sum = 0;
 #pragma unroll
     for (int j = 0; j < CH; ++j) sum += cj[j];
-    constexpr int SW = TPW < 64 ? TPW : 64;
-    const int lt = t & (SW - 1);
     int incl = sum;
 #pragma unroll
     for (int d = 1; d < SW; d <<= 1) {
@@ -758,9 +797,34 @@ __device__ __forceinline__ void phase_chunk(const cpx<double> *xrow, int t, doub
     int K = incl - sum;  // corrections of every bin < k0
     if constexpr (TPW >= 128) {  // add the totals of the window's earlier waves
         int *sb = reinterpret_cast<int *>(scanbuf + 8);
+        double *bhi = scanbuf + 16, *blo = scanbuf + 16 + G::NWV;  // kDpp: each wave's last / first phase
         if (lt == 63) sb[t >> 6] = incl;
+        if constexpr (kDpp) {
+            if (lt == 63) bhi[t >> 6] = ph[CH];
+            if (lt == 0) blo[t >> 6] = ph[1];
+        }
         __syncthreads();
-        for (int i = 0; i < (t >> 6); ++i) K += sb[i];
+        const int wv = t >> 6;
+        auto cw = [&](int i) {  // correction at wave i's first bin (i >= 1)
+            const double diff = blo[i] - bhi[i - 1];
+            return diff > kPi ? -1 : diff < -kPi ? 1 : 0;
+        };
+        for (int i = 0; i < wv; ++i) K += sb[i] + ((kDpp && i > 0) ? cw(i) : 0);
+        if constexpr (kDpp) {
+            if (wv > 0) {
+                if (lt == 0) {
+                    ph[0] = bhi[wv - 1];
+                    cj[0] = cw(wv);
+                } else {
+                    K += cw(wv);
+                }
+            }
+            if (wtail) {
+                ph[CH + 1] = blo[wv + 1];
+                const double diff = ph[CH + 1] - ph[CH];
+                cj[CH] = diff > kPi ? -1 : diff < -kPi ? 1 : 0;
+            }
+        }
     }
     const double um1 = fma((double)K, k2Pi, ph[0]);  // u[k0 - 1]
 #pragma unroll
@@ -956,7 +1020,9 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     // scan scratch: doubles [0, 8) wave totals of the mean / IIR reductions, [8, 16) the unwrap's
     // int wave totals; + (top-k with several waves per window) one sorted list per wave;
     // + (kOutTopKPhase) the winners of every window
+    // + (kOutPhase, several waves per window) each wave's first and last phase (phase_chunk's DPP exchange)
     constexpr int kScan = 16 * 8 + ((OUT == kOutTopK || OUT == kOutTopKPhase) && TPW >= 128 ? NWV * 64 * (8 + 4) : 0) +
+                          (OUT == kOutPhase && TPW >= 128 ? 2 * NWV * 8 : 0) +
                           (OUT == kOutTopKPhase ? WPB * (M < 64 ? M : 64) * 4 : 0);
     static_assert(!kPhase || sizeof(T) == 8, "phase outputs are fp64");
     constexpr bool kCosWin = WCLASS == kWinCos || WCLASS == kWinCos2;
@@ -1433,7 +1499,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
         if constexpr (OUT == kOutPhase && !kPhaseSplit) {
             const cpx<double> *xrow = reinterpret_cast<const cpx<double> *>(lbase);
             __syncthreads();  // X row complete
-            phase_chunk<LOG2N>(xrow, t, scanbuf, pw, u, gd);
+            phase_chunk<LOG2N, 16, false, true>(xrow, t, scanbuf, pw, u, gd);
             {
                 // record [P | unwrapped phase | group delay]: each row staged through this window's
                 // LDS slot (2 pad doubles per 16 keep pairs 16-B aligned and the lane-strided writes
