@@ -617,6 +617,8 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             HIP_OR(launch_slide_topk(A, s), MTB_INTERNAL_ERROR);
             return MTB_OK;
         }
+        A.trace = c.trace;  // power slide: workgroup b writes 4 entries at 4 b (diagnostic, wsp_plan_set_trace)
+        A.trace_cap = c.trace_cap;
         HIP_OR(launch_slide(A, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }

@@ -74,78 +74,6 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds_sub(d2 *buf
     }
 }
 
-// The same transform with the data in registers between passes (round 5): R = N / NT points per thread (8 at
-// N = 4096 / 2048, 4 at 1024 / 512 with two bins per thread), Stockham passes of radix R (the last one of the
-// remaining factor), the thread's pass-0 inputs x[t + NT r] straight from the caller's registers (no input
-// staging round trip), LDS only to exchange between passes.  N = 4096: 4 passes and 7 barriers instead of 6
-// radix-4 LDS passes, 12 barriers and the input staging -- the seeds were 14 % of every C5 task (33 of 242 us,
-// the r05c timeline) and all of the first round's latency.  Twiddles W_{Ns R}^k from the W_4096 quarter table
-// (k N / (Ns R) < N / 4 for R = 4 / 8; a final radix-2 pass folds its upper quarter by W^(N/4) = -i), their powers
-// by products (<= 7 steps).
-template <int LOG2N, int NT, int RP, int NS>
-__device__ __forceinline__ void reg_pass_write(d2 (&v)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
-    constexpr int N = 1 << LOG2N, R = N / NT, Q = R / RP, TS = 4096 / N;
-    static_assert(Q * RP == R && RP >= 2, "pass geometry");
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        const int j = t + NT * q, k = j & (NS - 1);
-        d2 *a = v + q * RP;
-        if constexpr (NS > 1) {
-            // W_N^m, m = k N / (Ns R): below N/4 (the quarter table) for R = 4 / 8; a last radix-2 pass reaches
-            // m < N/2, whose upper quarter is W_N^(m - N/4) (-i)
-            const int m = k * (N / (NS * RP));
-            d2 w;
-            if constexpr (RP == 2) {
-                const d2 q = twq[(m & (N / 4 - 1)) * TS];
-                w = m < N / 4 ? q : d2{q.y, -q.x};
-            } else {
-                w = twq[m * TS];
-            }
-            d2 wr = w;
-#pragma unroll
-            for (int r = 1; r < RP; ++r) {
-                a[r] = cmul(a[r], wr);
-                if (r + 1 < RP) wr = cmul(wr, w);
-            }
-        }
-        core::cpx<double> c[RP];  // by value: a d2 / cpx type pun through pointers breaks type-based alias analysis
-#pragma unroll
-        for (int r = 0; r < RP; ++r) c[r] = {a[r].x, a[r].y};
-        core::dft<double, RP>(c);
-#pragma unroll
-        for (int r = 0; r < RP; ++r) a[r] = d2{c[r].re, c[r].im};
-        const int o = (j - k) * RP + k;
-#pragma unroll
-        for (int r = 0; r < RP; ++r) buf[o + NS * r] = a[r];
-    }
-}
-template <int LOG2N, int NT, int NS>
-__device__ __forceinline__ void reg_passes(d2 *buf, const d2 *twq, int t) {
-    constexpr int N = 1 << LOG2N, R = N / NT;
-    if constexpr (NS < N) {
-        constexpr int RP = N / NS >= R ? R : N / NS;
-        d2 v[R];
-#pragma unroll
-        for (int q = 0; q < R / RP; ++q)
-#pragma unroll
-            for (int r = 0; r < RP; ++r) v[q * RP + r] = buf[t + NT * q + (N / RP) * r];
-        __syncthreads();
-        reg_pass_write<LOG2N, NT, RP, NS>(v, buf, twq, t);
-        __syncthreads();
-        reg_passes<LOG2N, NT, NS * RP>(buf, twq, t);
-    }
-}
-// a[r] = this thread's input x[t + NT r]; buf must be free (no reads pending).  Natural order in buf, ends after a
-// barrier.
-template <int LOG2N, int NT>
-__device__ __forceinline__ void fft_reg_sub(d2 (&a)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
-    constexpr int N = 1 << LOG2N, R = N / NT;
-    static_assert(R == 4 || R == 8, "4 or 8 points per thread");
-    reg_pass_write<LOG2N, NT, R, 1>(a, buf, twq, t);
-    __syncthreads();
-    reg_passes<LOG2N, NT, R>(buf, twq, t);
-}
-
 // The kernel argument is read in place through the kernarg segment pointer (address space 4: scalar loads, any
 // index).  Passing the struct by reference to the device functions made the compiler copy its 1.4 KiB to scratch.
 typedef const __attribute__((address_space(4))) SlideMix *MixP;
@@ -226,7 +154,7 @@ __device__ __forceinline__ void mix_task(MixP m, int c, int64_t task, d2 *lds, c
                 const double xi = on ? (double)x[i] - lvl : 0.0;
                 a[r] = mm == 0 ? d2{xi, 0.0} : xi * mod[(mm - 1) * N + i];
             }
-            fft_reg_sub<LOG2N, NT>(a, buf, twq, t);
+            fft_reg_sub<LOG2N, NT, 4096 / N>(a, buf, twq, t);
         } else {  // mode 5 (ablation): the round-4 form, inputs staged in LDS and radix-4 passes through LDS
             for (int i = t; i < N; i += NT) {
                 const double xi = on ? (double)x[i] - lvl : 0.0;

@@ -20,7 +20,7 @@
 // ~57 for the radix-16/8 FFT at N = 2048.  The mean detrend is linear:
 // X_w - mean_w * H[k], H = DFT of the window.
 //
-// Layout: one workgroup per segment of consecutive windows (32..256 windows, about two rounds of
+// Layout: one workgroup per segment of consecutive windows (32..128 windows since round 6: several rounds of
 // resident workgroups: launch_t), N/(2B) threads; thread t owns bins k = 2 (t + NT q) + e (q < B/2,
 // e < 2), so every store instruction of a wave writes 128 consecutive bins (1 KiB fp64) as one 16-B
 // store per lane.  The segment's trackers are SEEDED exactly, not slid from the previous segment:
@@ -112,6 +112,79 @@ template <int LOG2N, int NT> __device__ __forceinline__ void fft_lds(d2 *buf, co
     }
 }
 
+// The same transform with the data in registers between passes (round 5): R = N / NT points per thread (8 at
+// N = 4096 / 2048, 4 at 1024 / 512 with two bins per thread), Stockham passes of radix R (the last one of the
+// remaining factor), the thread's pass-0 inputs x[t + NT r] straight from the caller's registers (no input
+// staging round trip), LDS only to exchange between passes.  N = 4096: 4 passes and 7 barriers instead of 6
+// radix-4 LDS passes, 12 barriers and the input staging -- the seeds were 14 % of every C5 task (33 of 242 us,
+// the r05c timeline) and all of the first round's latency.  Twiddles W_{Ns R}^k from the W_4096 quarter table
+// (k N / (Ns R) < N / 4 for R = 4 / 8; a final radix-2 pass folds its upper quarter by W^(N/4) = -i), their powers
+// by products (<= 7 steps).  TS: the quarter table's stride for W_N (4096 / N for the mixed launch's W_4096 table,
+// 1 for slide_kernel's own W_N table, round 6).
+template <int LOG2N, int NT, int RP, int NS, int TS>
+__device__ __forceinline__ void reg_pass_write(d2 (&v)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT, Q = R / RP;
+    static_assert(Q * RP == R && RP >= 2, "pass geometry");
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = t + NT * q, k = j & (NS - 1);
+        d2 *a = v + q * RP;
+        if constexpr (NS > 1) {
+            // W_N^m, m = k N / (Ns R): below N/4 (the quarter table) for R = 4 / 8; a last radix-2 pass reaches
+            // m < N/2, whose upper quarter is W_N^(m - N/4) (-i)
+            const int m = k * (N / (NS * RP));
+            d2 w;
+            if constexpr (RP == 2) {
+                const d2 q = twq[(m & (N / 4 - 1)) * TS];
+                w = m < N / 4 ? q : d2{q.y, -q.x};
+            } else {
+                w = twq[m * TS];
+            }
+            d2 wr = w;
+#pragma unroll
+            for (int r = 1; r < RP; ++r) {
+                a[r] = cmul(a[r], wr);
+                if (r + 1 < RP) wr = cmul(wr, w);
+            }
+        }
+        core::cpx<double> c[RP];  // by value: a d2 / cpx type pun through pointers breaks type-based alias analysis
+#pragma unroll
+        for (int r = 0; r < RP; ++r) c[r] = {a[r].x, a[r].y};
+        core::dft<double, RP>(c);
+#pragma unroll
+        for (int r = 0; r < RP; ++r) a[r] = d2{c[r].re, c[r].im};
+        const int o = (j - k) * RP + k;
+#pragma unroll
+        for (int r = 0; r < RP; ++r) buf[o + NS * r] = a[r];
+    }
+}
+template <int LOG2N, int NT, int NS, int TS>
+__device__ __forceinline__ void reg_passes(d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT;
+    if constexpr (NS < N) {
+        constexpr int RP = N / NS >= R ? R : N / NS;
+        d2 v[R];
+#pragma unroll
+        for (int q = 0; q < R / RP; ++q)
+#pragma unroll
+            for (int r = 0; r < RP; ++r) v[q * RP + r] = buf[t + NT * q + (N / RP) * r];
+        __syncthreads();
+        reg_pass_write<LOG2N, NT, RP, NS, TS>(v, buf, twq, t);
+        __syncthreads();
+        reg_passes<LOG2N, NT, NS * RP, TS>(buf, twq, t);
+    }
+}
+// a[r] = this thread's input x[t + NT r]; buf must be free (no reads pending).  Natural order in buf, ends after a
+// barrier.
+template <int LOG2N, int NT, int TS>
+__device__ __forceinline__ void fft_reg_sub(d2 (&a)[(1 << LOG2N) / NT], d2 *buf, const d2 *twq, int t) {
+    constexpr int N = 1 << LOG2N, R = N / NT;
+    static_assert(R == 4 || R == 8, "4 or 8 points per thread");
+    reg_pass_write<LOG2N, NT, R, 1, TS>(a, buf, twq, t);
+    __syncthreads();
+    reg_passes<LOG2N, NT, R, TS>(buf, twq, t);
+}
+
 // Bin b of thread t: pairs of adjacent bins, 2 (t + NT (b / 2)) + b % 2, so that a wave's store of a pair
 // of powers is one 16-B access per lane (1 KiB contiguous per wave instruction).
 template <int NT> __device__ __forceinline__ int kbin_of(int t, int b) { return 2 * (t + NT * (b >> 1)) + (b & 1); }
@@ -131,14 +204,29 @@ __device__ __forceinline__ void seed_ffts(const SlideArgs &a, const T *__restric
         for (int i = t; i < N / 4; i += NT) twq[i] = tw[i];
         twl = twq;
     }
+    // round 6: with the quarter table in LDS (N <= 4096) the transforms run as register passes (fft_reg_sub, the
+    // mixed launch's seeds since round 5: N = 2048 in 4 passes and 7 barriers instead of a radix-2 stage, 5 radix-4
+    // LDS passes, 12 barriers and the input staging round trip), inputs straight from global memory into registers
+    // (twq is complete at the first pass's barrier: pass 0 uses no twiddles)
 #pragma unroll
     for (int m = 0; m <= NM; ++m) {
-        for (int i = t; i < N; i += NT) {
-            const double xi = (double)x[i] - lvl;
-            lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
+        if constexpr (TWL && (N / NT == 4 || N / NT == 8)) {
+            d2 v[N / NT];
+#pragma unroll
+            for (int r = 0; r < N / NT; ++r) {
+                const int i = t + NT * r;
+                const double xi = (double)x[i] - lvl;
+                v[r] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
+            }
+            fft_reg_sub<LOG2N, NT, 1>(v, lds, twl, t);
+        } else {
+            for (int i = t; i < N; i += NT) {
+                const double xi = (double)x[i] - lvl;
+                lds[i] = m == 0 ? d2{xi, 0.0} : xi * mod[(m - 1) * N + i];
+            }
+            __syncthreads();
+            fft_lds<LOG2N, NT>(lds, twl);
         }
-        __syncthreads();
-        fft_lds<LOG2N, NT>(lds, twl);
         pick(m, m == 0 ? a.s0 : (m == 1 ? a.s1 : a.s2), lds);
         __syncthreads();
     }
@@ -231,6 +319,16 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
     const T *__restrict__ x = static_cast<const T *>(sg.series) + sg.w0;  // the segment's first window
     const d2 *__restrict__ omega = static_cast<const d2 *>(a.omega);  // [NF][M]
     const d2 *__restrict__ hwin = omega + NF * M;                      // [M]
+    // diagnostic timeline (wsp_plan_set_trace, scripts/slide_timeline.py): workgroup b writes {block | XCC << 32,
+    // start, seeds done, end} at trace[4 b] while 4 b + 4 <= trace_cap; off (nullptr) by default
+    long long *trc = (a.trace && 4 * (int64_t)blockIdx.x + 4 <= a.trace_cap && threadIdx.x == 0)
+                         ? a.trace + 4 * (int64_t)blockIdx.x : nullptr;
+    if (trc) {
+        unsigned xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        trc[0] = (long long)blockIdx.x | ((long long)(xcc & 15) << 32);
+        trc[1] = wall_clock64();
+    }
 
     d2 om[B][NF], tr[B][NF];
     // mean detrend: the trackers follow x - L, L = the segment's first sample, and the output subtracts
@@ -254,6 +352,7 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
         if (DETREND == kDetrendMean && m == 0) sum0 = y[0].x;  // broadcast read: sum of x - L
     });
 
+    if (trc) trc[2] = wall_clock64();
 #pragma unroll
     for (int b = 0; b < B; ++b)
 #pragma unroll
@@ -319,6 +418,7 @@ __global__ __launch_bounds__((1 << LOG2N) / (2 * slide_b<LOG2N>()),
             if (c0 + st + 1 < len) slide_step<B, NF, DETREND>(tr, om, u + st * REC, sum);
         }
     }
+    if (trc) trc[3] = wall_clock64();
 }
 
 // Workgroups: each slides a segment of consecutive windows (seeded once, per-step uniforms staged CH
@@ -1062,10 +1162,25 @@ hipError_t launch_t(const SlideArgs &a0, const SlideGroup &g0, hipStream_t s) {
     SlideGroup g = g0;
     int64_t total = 0;
     for (int m = 0; m < g.n; ++m) total += g.n_windows[m];
-    if (a.seg <= 0) {  // one round of resident workgroups, 32..256 windows each (sweeps: DESIGN.md 4.5)
+    if (a.seg <= 0) {
+        // Round 6 (profiles/r06/c4_seg): 128-window segments from four rounds of them on, 64-window
+        // segments from one round of those on, below that one round of resident workgroups (>= 32 windows each).
+        // The round-2..5 policy -- one round of resident workgroups, at most 256 windows -- left a one-round launch
+        // (a 1/8 C4 shard: 767 workgroups of 171 windows) waiting for its slowest workgroups: workgroups with equal
+        // work ended between 107 and 222 us (slide_timeline, the older workgroups of a CU run ahead and the last one
+        // finishes alone).  With several rounds of shorter segments a CU whose workgroups finish early takes new
+        // ones.  Measured on C4 (N = 2048, Hann, 768 slots): whole batch 1.570 -> 1.482-1.520 ms at 128 (64: 1.527,
+        // 96-160: 1.57-1.63), 1/2 shard 0.797 -> 0.744 at 128, 1/4 0.408 -> 0.384 at 64, 1/8 0.220 -> 0.196-0.201 at
+        // 64 (48-144: 0.209-0.233).
         const int64_t slots = a.share > 1.0 ? (int64_t)((double)res / a.share) + 1 : (int64_t)res;
-        a.seg = (total + slots - 1) / slots;
-        a.seg = a.seg < 32 ? 32 : (a.seg > 256 ? 256 : a.seg);
+        if (total >= 4 * slots * 128) {
+            a.seg = 128;
+        } else if (total >= slots * 64) {
+            a.seg = 64;
+        } else {
+            a.seg = (total + slots - 1) / slots;
+            a.seg = a.seg < 32 ? 32 : a.seg;
+        }
     }
     g.blk0[0] = 0;
     for (int m = 0; m < g.n; ++m) g.blk0[m + 1] = g.blk0[m] + (g.n_windows[m] + a.seg - 1) / a.seg;

@@ -324,19 +324,18 @@ MTB_API int32_t wsp_plan_set_slide_segment(int64_t plan, int64_t windows);
  * (a chain's steps are staged in LDS).
  * MTB_BAD_ARGS for an unknown plan or segments outside 0..16. */
 MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
-/* Diagnostic: a timeline of the hop = 1 top-k kernels of later executes into
+/* Diagnostic: a timeline of the hop = 1 sliding-DFT kernels of later executes into
  * d_trace, a device buffer of `capacity` int64 (wall-clock ticks, 100 MHz):
  * seed workgroup b writes [b | XCC << 32, start, FFT m = 0 done, seeds done,
  * chain done, end] at 6 b and scan workgroup b [start, end] at capacity / 2 +
- * 2 b, each while it fits.  capacity = 0 turns it off (the default).
- * MTB_BAD_ARGS for an unknown plan or a null buffer. */
+ * 2 b, each while it fits; hop = 1 power slides (round 6): workgroup b writes
+ * [b | XCC << 32, start, seeds done, end] at 4 b.  capacity = 0 turns it off
+ * (the default).  MTB_BAD_ARGS for an unknown plan or a null buffer. */
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
 /* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
  * library's choice (default).  Same records within the parity bars either way.
  *  - hop = 1 power rows by the sliding DFT: 7 = plain stores (the default
  *    writes the rows through to memory, agent-scope sc1 stores);
- *  - fp32 Kalman pre-pass (two-segment form): 7 = its detrended rows written
- *    through to memory;
  *  - hop = 1 top-k records by the sliding DFT: 1 = one wave-wide reduction
  *    round per slot and window; 2 / 3 = the transposed lane-per-window scan
  *    (k <= 8, bands <= 256 bins) staging 16 / 8 windows per batch; 0 = the
