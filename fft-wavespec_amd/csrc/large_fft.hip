@@ -72,7 +72,11 @@ __global__ __launch_bounds__(CB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) 
     using G = LGeo<LOG2M2>;
     constexpr int M1 = 1 << LOG2M1, M2 = G::L, TP = G::TP, NB1 = M1 / CB;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    __shared__ cpx<T> lds[CB * G::SLOT];
+    // column c's transform at lds + c * CSTR: one complex of padding per column (round 6) -- at the unpadded stride
+    // (SLOT = M2 + M2/16 complex = a multiple of 32 dwords) the 8 lanes of a ds_write_b128 group (and the 16 of a
+    // ds_read_b128 group), which hold adjacent columns, all hit the same banks: 8-way conflicts on every exchange
+    constexpr int CSTR = G::SLOT + 1;
+    __shared__ cpx<T> lds[CB * CSTR];
     const int tid = threadIdx.x, c = tid % CB, t = tid / CB;
     const int beta = blockIdx.x % NB1;
     const int n1 = beta * CB + c;
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(CB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) 
             v[r] = {(T)xa, (T)xb};
         }
         if (kPrefetch && wc + wstep < a.nwin) load(wc + wstep);  // next window's samples in flight during this FFT
-        wg_fft<T, LOG2M2>(v, lds + c * G::SLOT, t, tw, a.log2n);
+        wg_fft<T, LOG2M2>(v, lds + c * CSTR, t, tw, a.log2n);
         // v[q R + r] = X[k2], k2 = t + TP q + (M2/R) r; twiddle W_M^(n1 k2) = W_N^(2 n1 k2)
         constexpr int R = last_radix<LOG2M2>();
         cpx<T> *__restrict__ yw = y + wc * (int64_t)M2 * M1;
@@ -164,6 +168,8 @@ struct RowArgs {
     int64_t w0, nwin;
     int log2n;
     int packed;      // 0: |X_k|^2 (N/2 per window); 1: out[2k] = Re X_k, out[2k+1] = Im X_k (N per window)
+    long long *trace;  // fused kernel diagnostic timeline (wsp_plan_set_trace), nullptr = off
+    int64_t trace_cap;
 };
 
 template <int LOG2M1> struct RowGeo {
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 // post-processing).  The workgroup's own stores of Y are visible to its loads after __syncthreads
 // (workgroup-scope release / acquire; one CU, one L1).
 template <typename T, int LOG2M1, int LOG2M2, int WCLASS, bool MEAN, bool PACKED, int NT = 256, bool PF = true,
-          bool NTS = false>
+          bool NTS = false, bool TR = false>
 __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     using GC = LGeo<LOG2M2>;
     using GR = LGeo<LOG2M1>;
@@ -290,7 +296,10 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     static_assert(CB * TPC == NT && 2 * RB * TPR == NT && NB1 >= 1 && NB2 >= 1, "thread geometry");
     constexpr int64_t M = (int64_t)M1 * M2;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    constexpr int LDS_C = CB * GC::SLOT, LDS_R = 2 * RB * GR::SLOT;
+    // column transforms at a stride of SLOT + 1 complex: adjacent columns (adjacent lanes) in different LDS banks
+    // (col_kernel; the column FFT took 8.5 of a column block's 13 us with the unpadded stride, r06o timeline)
+    constexpr int CSTR = GC::SLOT + 1;
+    constexpr int LDS_C = CB * CSTR, LDS_R = 2 * RB * GR::SLOT;
     __shared__ cpx<T> lds[LDS_C > LDS_R ? LDS_C : LDS_R];
     const int tid = threadIdx.x;
     const T *__restrict__ series = static_cast<const T *>(a.series);
@@ -332,12 +341,20 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
         sincos(a.inv_theta * (double)(2 * (cc + M1 * ct)), &sw00, &cw00);
         sincos(a.inv_theta * (double)(2 * CB), &sbd, &cbd);
     }
+    // diagnostic timeline (wsp_plan_set_trace, scripts/large_timeline.py): thread 0 of workgroup b records, for its
+    // first window only, 4 ticks per block -- start, samples / rows in registers (loads done), FFT done, block done --
+    // for the NB1 column blocks then the NB2 row blocks, at trace[32 b + 4 i] (NB1 + NB2 <= 8 blocks)
+    // (TR: a separate instantiation, so that the default kernel carries none of it)
+    long long *trc = (TR && ra.trace && threadIdx.x == 0 && 32 * (int64_t)blockIdx.x + 32 <= ra.trace_cap)
+                         ? ra.trace + 32 * (int64_t)blockIdx.x : nullptr;
     for (int64_t w = blockIdx.x; w < a.nwin; w += gridDim.x) {
+        if (w != blockIdx.x) trc = nullptr;
         // ---- column pass: NB1 blocks of CB columns
         if (PF) load_cols(w, 0);
         const double mean = MEAN ? a.means[w] : 0.0;
         double cwb = cw00, swb = sw00;  // angle of column block beta
         for (int beta = 0; beta < NB1; ++beta) {
+            if (trc && beta < 8) trc[4 * beta] = wall_clock64();
             if (!PF) load_cols(w, beta);
             const int n1 = beta * CB + cc;
             double cw = cwb, sw = swb;
@@ -375,9 +392,17 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 }
                 v[r] = {(T)xa, (T)xb};
             }
+            if (trc && beta < 8) {  // samples consumed: loads done
+                asm volatile("" ::"v"(v[15].re));
+                trc[4 * beta + 1] = wall_clock64();
+            }
             // next block's samples in flight during this FFT (not across the row pass: registers)
             if (PF && beta + 1 < NB1) load_cols(w, beta + 1);
-            wg_fft<T, LOG2M2>(v, lds + cc * GC::SLOT, ct, tw, a.log2n);
+            wg_fft<T, LOG2M2>(v, lds + cc * CSTR, ct, tw, a.log2n);
+            if (trc && beta < 8) {
+                asm volatile("" ::"v"(v[15].re));
+                trc[4 * beta + 2] = wall_clock64();
+            }
             constexpr int R = last_radix<LOG2M2>();
             const cpx<T> wstep_r = tw[(2 * n1 * (M2 / R)) & (N - 1)];
 #pragma unroll
@@ -390,11 +415,14 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                     if (r + 1 < R) wr = cmul(wr, wstep_r);
                 }
             }
+            if (trc && beta < 8) trc[4 * beta + 3] = wall_clock64();
         }
         __syncthreads();  // Y of this window complete and visible to the workgroup
         // ---- row pass: NB2 blocks of RB rows + their mirror rows
         if (PF) load_rows(0);
         for (int beta2 = 0; beta2 < NB2; ++beta2) {
+            const int ti = 4 * (NB1 + beta2);
+            if (trc && ti + 3 < 32) trc[ti] = wall_clock64();
             if (!PF) load_rows(beta2);
             const int i = rho < RB ? rho : rho - RB, lo = beta2 * RB + i;
             const int row = rho < RB ? lo : (lo == 0 ? M2 / 2 : M2 - lo);
@@ -402,8 +430,16 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
             cpx<T> v[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = nxt[r];
+            if (trc && ti + 3 < 32) {
+                asm volatile("" ::"v"(v[15].re));  // the rows are in registers
+                trc[ti + 1] = wall_clock64();
+            }
             if (PF && beta2 + 1 < NB2) load_rows(beta2 + 1);
             wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
+            if (trc && ti + 3 < 32) {
+                asm volatile("" ::"v"(v[15].re));
+                trc[ti + 2] = wall_clock64();
+            }
             constexpr int R = last_radix<LOG2M1>();
 #pragma unroll
             for (int q = 0; q < 16 / R; ++q)
@@ -460,6 +496,7 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 }
             }
             __syncthreads();
+            if (trc && ti + 3 < 32) trc[ti + 3] = wall_clock64();
         }
     }
 }
@@ -631,6 +668,13 @@ hipError_t fused_launch(const LargeLaunch &L, const large::ColArgs &ca0, const l
     const int per_cu = 1;
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>({L.n_windows, L.chunk, (int64_t)per_cu * cu_count()}));
     using namespace core;
+    if constexpr (sizeof(T) == 8 && NT == 512 && !PF && NTS) {  // diagnostic timeline of the default form (Hann, power)
+        if (ra.trace && !mean && !L.packed && wclass == kWinCos) {
+            hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, kWinCos, false, false, NT, PF, NTS, true>), dim3((unsigned)grid),
+                               dim3(NT), 0, s, ca, ra);
+            return hipGetLastError();
+        }
+    }
 #define FUSED(WC)                                                                                                          \
     if (mean) {                                                                                                            \
         if (L.packed) hipLaunchKernelGGL((large::fused_kernel<T, LM1, 8, WC, true, true, NT, PF, NTS>), dim3((unsigned)grid), dim3(NT), 0, s, ca, ra); \
@@ -754,6 +798,8 @@ template <typename T> hipError_t launch_t(const LargeLaunch &L, hipStream_t s) {
     ra.packed = L.packed;
     ra.w0 = 0;
     ra.nwin = L.n_windows;
+    ra.trace = L.trace;
+    ra.trace_cap = L.trace_cap;
     // The fused one-workgroup-per-window form (fused_kernel, 512 threads, no register prefetch) is the default
     // for fp64 N = 65536, the legacy default window (4096 x 65536: 1.387 ms against 1.444 for the two-pass form,
     // profiles/r03/s2); N = 131072 would hold 192 slots of 1 MiB at most (a quarter of the CUs idle) and stays

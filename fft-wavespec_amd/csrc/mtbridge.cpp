@@ -589,6 +589,8 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         G.packed = c.output == MTB_OUT_PACKED;
         G.f32 = c.f32;
         G.variant = c.variant;
+        G.trace = c.trace;
+        G.trace_cap = c.trace_cap;
         HIP_OR(launch_large(G, s), MTB_INTERNAL_ERROR);
         return MTB_OK;
     }

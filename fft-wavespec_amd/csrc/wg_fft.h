@@ -41,6 +41,13 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
     if constexpr (PASS < G::NP) {
         // write the previous pass's outputs: butterfly b (Ns = ns(PASS-1), R = radix(PASS-1))
         constexpr int Rp = G::radix(PASS - 1), Nsp = G::ns(PASS - 1);
+        constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
+        // twiddle W_{Ns R}^{j r} = W_N^{j r N/(Ns R)}: one table entry per butterfly, powers by products (<= 15
+        // steps: ~15 ulp).  Loaded before the exchange's barrier (round 6): behind it the table read's L2 latency
+        // was exposed on every pass (the barrier also orders global loads).
+        cpx<T> w1s[16 / R];
+#pragma unroll
+        for (int q = 0; q < 16 / R; ++q) w1s[q] = tw[(((t + TP * q) % Ns) << log2tw) / (Ns * R)];
 #pragma unroll
         for (int q = 0; q < 16 / Rp; ++q) {
             const int b = t + TP * q, j = b % Nsp, base = (b / Nsp) * Nsp * Rp + j;
@@ -48,15 +55,12 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
             for (int r = 0; r < Rp; ++r) slot[pad16(base + Nsp * r)] = v[q * Rp + r];
         }
         __syncthreads();
-        constexpr int R = G::radix(PASS), Ns = G::ns(PASS);
 #pragma unroll
         for (int q = 0; q < 16 / R; ++q) {
-            const int b = t + TP * q, j = b % Ns;
+            const int b = t + TP * q;
 #pragma unroll
             for (int r = 0; r < R; ++r) v[q * R + r] = slot[pad16(b + (L / R) * r)];
-            // twiddle W_{Ns R}^{j r} = W_N^{j r N/(Ns R)}: one table entry, powers by products
-            // (<= 15 steps: ~15 ulp)
-            const cpx<T> w1 = tw[(j << log2tw) / (Ns * R)];
+            const cpx<T> w1 = w1s[q];
             cpx<T> wr = w1;
 #pragma unroll
             for (int r = 1; r < R; ++r) {

@@ -83,6 +83,8 @@ struct LargeLaunch {
     int packed;           // 0 power, 1 packed (Re, Im)
     bool f32;
     double iir_alpha, iir_c;
+    long long *trace;     // diagnostic (wsp_plan_set_trace): fused kernel, workgroup b's first window -> 32 ticks at 32 b
+    int64_t trace_cap;
     int variant;          // wsp_plan_set_variant (include/mtbridge.h): 0 = the library's choice (fused non-temporal kernel for
                           // fp64 N = 65536, two passes otherwise), 1 two passes, 2 two passes pipelined over two streams,
                           // 3 fused (512 threads), 4 fused (256 threads, register prefetch), 5 fused with plain stores,

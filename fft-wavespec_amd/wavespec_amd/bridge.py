@@ -349,7 +349,8 @@ class Plan:
         _check("wsp_plan_set_seed_chain", lib().wsp_plan_set_seed_chain(self.handle, segments))
 
     def set_trace(self, d_trace: int, capacity: int) -> None:
-        """Diagnostic: timeline of the hop = 1 top-k kernels into a device buffer of `capacity` int64."""
+        """Diagnostic: timeline of the hop = 1 slide / top-k kernels or the fused large-N kernel into a device buffer
+        of `capacity` int64 (include/mtbridge.h wsp_plan_set_trace)."""
         _check("wsp_plan_set_trace", lib().wsp_plan_set_trace(self.handle, d_trace, capacity))
 
     def set_variant(self, variant: int) -> None:
