@@ -441,6 +441,10 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 trc[ti + 2] = wall_clock64();
             }
             constexpr int R = last_radix<LOG2M1>();
+            // the R2C step's twiddles, loaded before the barrier (round 6: behind it their L2 latency was exposed)
+            cpx<T> wk0[16 / R];
+#pragma unroll
+            for (int q = 0; q < 16 / R; ++q) wk0[q] = tw[(row + M2 * (rt + TPR * q)) & (N - 1)];
 #pragma unroll
             for (int q = 0; q < 16 / R; ++q)
 #pragma unroll
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
             const cpx<T> wstep_r = tw[(M2 * (M1 / R)) & (N - 1)];
 #pragma unroll
             for (int q = 0; q < 16 / R; ++q) {
-                cpx<T> wk = tw[(row + M2 * (rt + TPR * q)) & (N - 1)];
+                cpx<T> wk = wk0[q];
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int k1 = rt + TPR * q + (M1 / R) * r;
