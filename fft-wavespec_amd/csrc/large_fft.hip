@@ -72,11 +72,12 @@ __global__ __launch_bounds__(CB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) 
     using G = LGeo<LOG2M2>;
     constexpr int M1 = 1 << LOG2M1, M2 = G::L, TP = G::TP, NB1 = M1 / CB;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    // column c's transform at lds + c * CSTR: one complex of padding per column (round 6) -- at the unpadded stride
-    // (SLOT = M2 + M2/16 complex = a multiple of 32 dwords) the 8 lanes of a ds_write_b128 group (and the 16 of a
-    // ds_read_b128 group), which hold adjacent columns, all hit the same banks: 8-way conflicts on every exchange
-    constexpr int CSTR = G::SLOT + 1;
-    __shared__ cpx<T> lds[CB * CSTR];
+    // the CB column transforms interleaved element by element (wg_fft stride S = CB, round 6): with one contiguous
+    // slot per column (SLOT = M2 + M2/16 complex = a multiple of 32 dwords) the 8 lanes of a ds_write_b128 group and
+    // the 16 of a ds_read_b128 group, which hold adjacent columns, all hit the same banks (8-way conflicts on every
+    // exchange); one element of padding per column still left 2-3-way read conflicts at CB = 8 / 16 (SQ pass r06s:
+    // 0.40 of the col_kernel's LDS cycles at N = 262144)
+    __shared__ cpx<T> lds[CB * G::SLOT];
     const int tid = threadIdx.x, c = tid % CB, t = tid / CB;
     const int beta = blockIdx.x % NB1;
     const int n1 = beta * CB + c;
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(CB *(1 << LOG2M2) / 16) void col_kernel(ColArgs a) 
             v[r] = {(T)xa, (T)xb};
         }
         if (kPrefetch && wc + wstep < a.nwin) load(wc + wstep);  // next window's samples in flight during this FFT
-        wg_fft<T, LOG2M2>(v, lds + c * CSTR, t, tw, a.log2n);
+        wg_fft<T, LOG2M2, 1, CB>(v, lds + c, t, tw, a.log2n);
         // v[q R + r] = X[k2], k2 = t + TP q + (M2/R) r; twiddle W_M^(n1 k2) = W_N^(2 n1 k2)
         constexpr int R = last_radix<LOG2M2>();
         cpx<T> *__restrict__ yw = y + wc * (int64_t)M2 * M1;
@@ -296,10 +297,10 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
     static_assert(CB * TPC == NT && 2 * RB * TPR == NT && NB1 >= 1 && NB2 >= 1, "thread geometry");
     constexpr int64_t M = (int64_t)M1 * M2;
     constexpr bool kCos = WCLASS == core::kWinCos || WCLASS == core::kWinCos2;
-    // column transforms at a stride of SLOT + 1 complex: adjacent columns (adjacent lanes) in different LDS banks
-    // (col_kernel; the column FFT took 8.5 of a column block's 13 us with the unpadded stride, r06o timeline)
-    constexpr int CSTR = GC::SLOT + 1;
-    constexpr int LDS_C = CB * CSTR, LDS_R = 2 * RB * GR::SLOT;
+    // column transforms interleaved element by element (wg_fft stride S = CB; col_kernel): adjacent columns (adjacent
+    // lanes) in different LDS banks -- the column FFT took 8.5 of a column block's 13 us with contiguous per-column
+    // slots (r06o timeline), 4.3-4.7 with one element of padding per column (r06p)
+    constexpr int LDS_C = CB * GC::SLOT, LDS_R = 2 * RB * GR::SLOT;
     __shared__ cpx<T> lds[LDS_C > LDS_R ? LDS_C : LDS_R];
     const int tid = threadIdx.x;
     const T *__restrict__ series = static_cast<const T *>(a.series);
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
             }
             // next block's samples in flight during this FFT (not across the row pass: registers)
             if (PF && beta + 1 < NB1) load_cols(w, beta + 1);
-            wg_fft<T, LOG2M2>(v, lds + cc * CSTR, ct, tw, a.log2n);
+            wg_fft<T, LOG2M2, 1, CB>(v, lds + cc, ct, tw, a.log2n);
             if (trc && beta < 8) {
                 asm volatile("" ::"v"(v[15].re));
                 trc[4 * beta + 2] = wall_clock64();

@@ -33,7 +33,13 @@ template <int LOG2L> struct LGeo {
 // v[r] = x[t + TP r] on entry).  On exit v[q R + r] = X[b + (L/R) r] with
 // b = t + TP q and R the last pass's radix.  `slot` is this transform's LDS
 // region (SLOT elements); tw = W_N^j, j < N, of a table of period N (twN).
-template <typename T, int LOG2L, int PASS = 1>
+// S: element stride of the transform in LDS (round 6).  S = 1: the transform owns SLOT consecutive elements.  S = CB > 1:
+// CB transforms interleaved element by element (element e of transform c at slot_base[c + CB pad16(e)], the caller
+// passing slot = base + c): the lanes of one LDS instruction, which hold adjacent transforms at nearby elements, then
+// fall on distinct banks for every pass (the column passes of large_fft.hip; contiguous per-column slots a multiple
+// of 32 dwords apart made them 8-way conflicts, and a one-element pad still left 2-3-way read conflicts at 8 or 16
+// columns per workgroup).
+template <typename T, int LOG2L, int PASS = 1, int S = 1>
 __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, const cpx<T> *__restrict__ tw, int log2tw) {
     using G = LGeo<LOG2L>;
     constexpr int L = G::L, TP = G::TP;
@@ -52,14 +58,14 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
         for (int q = 0; q < 16 / Rp; ++q) {
             const int b = t + TP * q, j = b % Nsp, base = (b / Nsp) * Nsp * Rp + j;
 #pragma unroll
-            for (int r = 0; r < Rp; ++r) slot[pad16(base + Nsp * r)] = v[q * Rp + r];
+            for (int r = 0; r < Rp; ++r) slot[S * pad16(base + Nsp * r)] = v[q * Rp + r];
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 16 / R; ++q) {
             const int b = t + TP * q;
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[q * R + r] = slot[pad16(b + (L / R) * r)];
+            for (int r = 0; r < R; ++r) v[q * R + r] = slot[S * pad16(b + (L / R) * r)];
             const cpx<T> w1 = w1s[q];
             cpx<T> wr = w1;
 #pragma unroll
@@ -70,7 +76,7 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
             dft<T, R>(v + q * R);
         }
         __syncthreads();  // slot reuse by the caller / next pass
-        wg_fft<T, LOG2L, PASS + 1>(v, slot, t, tw, log2tw);
+        wg_fft<T, LOG2L, PASS + 1, S>(v, slot, t, tw, log2tw);
     }
 }
 
