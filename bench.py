@@ -262,14 +262,20 @@ def cpu_baseline(d_series, cfg: dict, budget_s: float, threads: int = 1) -> dict
 
 
 def load_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/traffic.json), or None; the pass's
+    source directory (prof_<tag>_<key>) is kept beside it for the line's traffic_source."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
     try:
-        return json.loads(p.read_text()).get(config, {}).get("hbm_bytes_per_launch")
+        e = json.loads(p.read_text()).get(config, {})
     except Exception:
         return None
+    TRAFFIC_SOURCE[config] = e.get("source")
+    return e.get("hbm_bytes_per_launch")
+
+
+TRAFFIC_SOURCE = {}
 
 
 def load_valu(config: str):
@@ -633,7 +639,10 @@ def main(argv=None):
             "roofline": {"bound": "valu" if wl.valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
                          "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a "
-                                           "separate run, scripts/parse_prof.py), not this run" if wl.traffic else None,
+                                           "separate run of the same command, scripts/parse_prof.py"
+                                           + (f", {next(v for v in TRAFFIC_SOURCE.values() if v)}"
+                                              if any(TRAFFIC_SOURCE.values()) else "")
+                                           + "), not this run" if wl.traffic else None,
                          **({"valu": wl.valu, "note": "VALU-issue-bound: achieved / frac are the HBM roofline, "
                                                       "valu.issue_frac the bound's"} if wl.valu else {}),
                          "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,

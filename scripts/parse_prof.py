@@ -73,6 +73,7 @@ if fetch is not None and write is not None:
     res["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; all our kernels' dispatches "
                      "summed per main (spectrum/inverse) dispatch; read = FETCH_SIZE*1024*2 (gfx950 half-count "
                      "correction), write = WRITE_SIZE*1024")
+res["source"] = out.name  # the gpurun_out directory of the passes (gpu_profile.sh: prof_<tag>_<key>)
 print(json.dumps(res, indent=1))
 tj = Path("profiles/traffic.json")
 allres = json.loads(tj.read_text()) if tj.exists() else {}
