@@ -1012,7 +1012,13 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     constexpr int R0 = G::R0, BPT0 = G::BPT0;
     constexpr bool kPrefetch = !(VAR & kVarNoPrefetch);
     constexpr int kSplit = (VAR & kVarSplitLds) ? ((VAR & kVarLdsB64) ? 2 : 1) : 0;
-    constexpr int kCplx = WPB * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));
+    // per-window LDS slot: the exchange's SLOT elements; the AoS phase record (round 6) stages two of its three rows
+    // at once, 2 x (M + M/8) doubles, slightly more than the exchange's SLOT complex (occupancy unchanged: 4
+    // workgroups per CU at N = 4096 either way)
+    constexpr int kSlotB = (OUT == kOutPhase && !kSplit && 2 * (M + M / 8) * 8 > SLOT * (int)sizeof(cpx<T>))
+                               ? 2 * (M + M / 8) * 8
+                               : SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));
+    constexpr int kCplx = WPB * kSlotB;
     constexpr int kRaw = DETREND == kDetrendIir ? WPB * (N + N / 32) * 8 : 0;
     constexpr int kMain = kCplx > kRaw ? kCplx : kRaw;
     constexpr bool kPhase = OUT == kOutPhase || OUT == kOutTopKPhase;
@@ -1032,7 +1038,7 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
     const int tid = threadIdx.x;
     const int slot = tid / TPW;
     int t = tid % TPW;  // re-pinned per window in the split top-k + phase form (below)
-    char *lbase = smem + slot * SLOT * (int)(kSplit ? sizeof(T) : sizeof(cpx<T>));  // this window's LDS slot
+    char *lbase = smem + slot * kSlotB;  // this window's LDS slot
 
     // per-thread window rotation start: th_i at i = 2 (t + TPW q)
     double wc0[BPT0], ws0[BPT0];
@@ -1522,8 +1528,29 @@ __global__ __launch_bounds__((Blk<LOG2N, VAR>::BLOCK),(VAR & kVarSplitLds) ? ((V
                         }
                     }
                 };
-                put(pw, 0);
-                put(u, 1);
+                // the power and phase rows staged together (round 6: one barrier pair fewer per window), then the
+                // group delay
+                {
+                    constexpr int RW = M + M / 8;  // doubles per staged row (pidx(M))
+                    __syncthreads();  // the X reads of phase_chunk are done
+#pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        *reinterpret_cast<v2 *>(srow + pidx(16 * t + j)) = v2{pw[j], pw[j + 1]};
+                        *reinterpret_cast<v2 *>(srow + RW + pidx(16 * t + j)) = v2{u[j], u[j + 1]};
+                    }
+                    __syncthreads();
+                    if (active) {
+                        T *dst = a.out + w * (int64_t)(3 * M);
+#pragma unroll
+                        for (int r = 0; r < 2; ++r)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const int k = 2 * (t + TPW * j);
+                                __builtin_nontemporal_store(*reinterpret_cast<const v2 *>(srow + r * RW + pidx(k)),
+                                                            reinterpret_cast<v2 *>(dst + r * M + k));
+                            }
+                    }
+                }
                 put(gd, 2);
             }
         }
