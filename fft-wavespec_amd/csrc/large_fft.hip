@@ -214,7 +214,10 @@ __global__ __launch_bounds__(2 * RowGeo<LOG2M1>::RB *(1 << LOG2M1) / 16) void ro
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = nxt[r];
         if (wc + wstep < a.nwin) load(wc + wstep);  // next window's rows in flight during this one
-        wg_fft<T, LOG2M1>(v, slot, t, tw, a.log2n);
+        // the row's TP threads are lanes of one wave and its slot is theirs: wave-local exchanges (round 6; N = 131072
+        // 1.378 -> 1.353-1.368 ms, 262144 1.641 -> 1.633, r06x same box)
+        static_assert(TP <= 64 && 64 % TP == 0, "a row's threads in one wave");
+        wg_fft<T, LOG2M1, 1, 1, true>(v, slot, t, tw, a.log2n);
         // Z[row + M2 k1] in v[q R + r], k1 = t + TP q + (M1/R) r: to LDS in natural order
         constexpr int R = last_radix<LOG2M1>();
 #pragma unroll
@@ -436,6 +439,8 @@ __global__ __launch_bounds__(NT) void fused_kernel(ColArgs a, RowArgs ra) {
                 trc[ti + 1] = wall_clock64();
             }
             if (PF && beta2 + 1 < NB2) load_rows(beta2 + 1);
+            // (workgroup barriers: the wave-local exchanges that the two-pass row kernel takes measured 1.186 -> 1.200
+            // ms here, r06x; profiles/r06/large/r06x_ab_wave_local_rows.log)
             wg_fft<T, LOG2M1>(v, slot, rt, tw, a.log2n);
             if (trc && ti + 3 < 32) {
                 asm volatile("" ::"v"(v[15].re));

@@ -39,7 +39,20 @@ template <int LOG2L> struct LGeo {
 // fall on distinct banks for every pass (the column passes of large_fft.hip; contiguous per-column slots a multiple
 // of 32 dwords apart made them 8-way conflicts, and a one-element pad still left 2-3-way read conflicts at 8 or 16
 // columns per workgroup).
-template <typename T, int LOG2L, int PASS = 1, int S = 1>
+// WL (round 6): the transform's TP threads are lanes of one wave and its slot is private to them (the row transforms
+// of large_fft.hip: 8 / 16 threads per row), so the exchanges only need the wave's own LDS ordering -- LDS executes a
+// wave's instructions in order; the wait and the memory clobber keep the compiler from moving the reads above the
+// writes -- instead of workgroup barriers that wait for every other wave.
+template <bool WL> __device__ __forceinline__ void wg_sync() {
+    if constexpr (WL) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
+template <typename T, int LOG2L, int PASS = 1, int S = 1, bool WL = false>
 __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, const cpx<T> *__restrict__ tw, int log2tw) {
     using G = LGeo<LOG2L>;
     constexpr int L = G::L, TP = G::TP;
@@ -60,7 +73,7 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
 #pragma unroll
             for (int r = 0; r < Rp; ++r) slot[S * pad16(base + Nsp * r)] = v[q * Rp + r];
         }
-        __syncthreads();
+        wg_sync<WL>();
 #pragma unroll
         for (int q = 0; q < 16 / R; ++q) {
             const int b = t + TP * q;
@@ -75,8 +88,8 @@ __device__ __forceinline__ void wg_fft(cpx<T> (&v)[16], cpx<T> *slot, int t, con
             }
             dft<T, R>(v + q * R);
         }
-        __syncthreads();  // slot reuse by the caller / next pass
-        wg_fft<T, LOG2L, PASS + 1, S>(v, slot, t, tw, log2tw);
+        wg_sync<WL>();  // slot reuse by the caller / next pass
+        wg_fft<T, LOG2L, PASS + 1, S, WL>(v, slot, t, tw, log2tw);
     }
 }
 
