@@ -329,7 +329,10 @@ MTB_API int32_t wsp_plan_set_seed_chain(int64_t plan, int32_t segments);
  * seed workgroup b writes [b | XCC << 32, start, FFT m = 0 done, seeds done,
  * chain done, end] at 6 b and scan workgroup b [start, end] at capacity / 2 +
  * 2 b, each while it fits; hop = 1 power slides (round 6): workgroup b writes
- * [b | XCC << 32, start, seeds done, end] at 4 b.  capacity = 0 turns it off
+ * [b | XCC << 32, start, seeds done, end] at 4 b; the fused large-N kernel
+ * (round 6: fp64 power with a Hann window, the N = 65536 default form) has
+ * workgroup b write, for its first window, 4 ticks per column / row block
+ * (start, loads done, FFT done, block done) at 32 b.  capacity = 0 turns it off
  * (the default).  MTB_BAD_ARGS for an unknown plan or a null buffer. */
 MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity);
 /* Tuning / ablation: the kernel form, 0..8 (MTB_BAD_ARGS outside); 0 = the
