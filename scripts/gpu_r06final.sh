@@ -1,7 +1,7 @@
 # round-6 closing check, in parts that each fit one gpurun call (gpu_run.sh stops at the first failing step):
 #   PART=a  the whole GPU suite, smoke, the default bench line (the driver's command), then the north-star kernel
 #           trace + PMC passes on the same lease
-#   PART=b  every configuration's line WITH the CPU baseline beside it (1 core + the job's cores)
+#   PART=b  every configuration's line WITH the CPU baseline beside it (the oracle on 1 core)
 #   PART=c  strong-scaling shards emulated one rank at a time (G = 2, 4, 8; each rank the median of 3 passes)
 set -u
 cd "$GRAFT_REPO_ROOT"
