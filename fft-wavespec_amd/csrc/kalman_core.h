@@ -539,6 +539,113 @@ __device__ __forceinline__ kf2 kstep_pk2(KState2 &st, const KConst<float> &c, kf
     return st.pos;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same step in the Newton (forward-difference) basis, the fp32 default since round 6.
+//
+// F = exp(N) (N the shift) is similar to the Jordan block Jd = I + N: F = T Jd T^-1 with
+//   T^-1 = [[1, 0, 0, 0], [0, 1, 1/2, 1/6], [0, 0, 1, 1], [0, 0, 0, 1]],
+// i.e. u = T^-1 x holds the forward differences of the cubic (u0 = pos, u1 = vel + acc/2 +
+// jerk/6, u2 = acc + jerk, u3 = jerk).  In u the state predict is three neighbour sums and the
+// covariance predict P' <- Jd P' Jd^T fifteen adds (instead of 6 and 35 operations); T's first
+// row is e0, so S, gain, boost, clip and the normalised update keep their form.  What the
+// reference adds beyond F P F^T carries over as:
+//  * the P11 prediction of :2052 adds e = P12 + P22 + (P13 + P23)/2 of the ORIGINAL basis; T^-1 e1
+//    = e1, so in u it is e added to P'11, e = P'12 - P'13/2 + P'22/2 - 11/12 P'23 + P'33/3;
+//  * Q = diag(Qp, Qv, Qa, Qj) becomes Q' = T^-1 Q T^-T: Qp on 00 plus six entries of the 1..3 block
+//    (KNb below), boosted as a whole by b = 1 + min(5, |y|/sigma) adapt;
+//  * the diagonal floors max(1e-12, P_ii) (:2110-2114) act on the original basis and are NOT
+//    applied.  Instead they are proven no-ops: while e >= -Qv/2 at every step, the predicted P
+//    dominates diag(Qp, Qv/2, Qa, Qj) (F P F^T and bQ are PSD, e e1e1^T takes at most Qv/2), so the
+//    updated P = (P_p^-1 + e0 e0^T/R)^-1 >= diag(Qp R/(Qp + R), Qv/2, Qa, Qj) -- above 1e-12 by the
+//    host's gate (nb2_ok: all of them >= 2^-20, far above fp32 rounding of P).  The kernel keeps
+//    min(e) per lane (one v_min3 per two steps and segment) and a wave with e < -Qv/2 anywhere
+//    re-runs in the original basis with the floors (kalman_pk2_kernel NB = false).
+// CPU model and checks of the algebra against the oracle: tests/test_kalman_newton.py.
+struct KNb {
+    float Qp, Q11, Q12, Q13, Q22, Q23, Q33, R, QpR, adapt, clip, emin;  // emin: -Qv/2
+};
+inline bool nb2_ok(const KP &kp) {
+    const double qs = kp.follow > 0.05 ? kp.follow : 0.05;
+    auto fl = [](double v) { return v > 1e-9 ? v : 1e-9; };
+    const double Qp = fl(kp.qp * qs), Qv = fl(kp.qv * qs), Qa = fl(kp.qa * qs), Qj = fl(kp.qj * qs), R = fl(kp.r);
+    double m = Qp * R / (Qp + R);
+    m = m < Qv / 2 ? m : Qv / 2;
+    m = m < Qa ? m : Qa;
+    m = m < Qj ? m : Qj;
+    return m >= 0x1p-20;
+}
+__device__ __forceinline__ KNb knb_const(const KP &kp) {
+    const double qs = fmax(0.05, kp.follow);
+    const double Qp = fmax(1e-9, kp.qp * qs), Qv = fmax(1e-9, kp.qv * qs), Qa = fmax(1e-9, kp.qa * qs),
+                 Qj = fmax(1e-9, kp.qj * qs), R = fmax(1e-9, kp.r);
+    KNb c;
+    c.Qp = (float)Qp;
+    c.Q11 = (float)(Qv + Qa / 4 + Qj / 36);
+    c.Q12 = (float)(Qa / 2 + Qj / 6);
+    c.Q13 = (float)(Qj / 6);
+    c.Q22 = (float)(Qa + Qj);
+    c.Q23 = (float)Qj;
+    c.Q33 = (float)Qj;
+    c.R = (float)R;
+    c.QpR = (float)(Qp + R);
+    c.adapt = (float)kp.adapt;
+    c.clip = (float)kp.clip;
+    c.emin = (float)(-0.5 * Qv);
+    return c;
+}
+// ResetKalmanState :2015-2029 in u (centred: u0 = 0): u = T^-1 (0, iv, ia, ij), P' = T^-1 P0 T^-T
+__device__ __forceinline__ void knb_reset(KState2 &st, const KP &kp) {
+    const double vp = fmax(1e-9, kp.vp), vv = fmax(1e-9, kp.vv), va = fmax(1e-9, kp.va), vj = fmax(1e-9, kp.vj);
+    auto b = [](double v) { const float f = (float)v; return kf2{f, f}; };
+    st.pos = kf2{0.f, 0.f};
+    st.vel = b(kp.iv + kp.ia / 2 + kp.ij / 6);
+    st.acc = b(kp.ia + kp.ij);
+    st.jerk = b(kp.ij);
+    st.p00 = b(vp);
+    st.p01 = st.p02 = st.p03 = kf2{0.f, 0.f};
+    st.p11 = b(vv + va / 4 + vj / 36);
+    st.p12 = b(va / 2 + vj / 6);
+    st.p13 = b(vj / 6);
+    st.p22 = b(va + vj);
+    st.p23 = b(vj);
+    st.p33 = b(vj);
+}
+// One step of both segments in u; e (the reference's P11 term) leaves through `e` for the guard.
+__device__ __forceinline__ kf2 kstep_nb2(KState2 &st, const KNb &c, kf2 z, kf2 &e) {
+    const kf2 p00 = st.p00, p01 = st.p01, p02 = st.p02, p03 = st.p03, p11 = st.p11, p12 = st.p12, p13 = st.p13,
+              p22 = st.p22, p23 = st.p23, p33 = st.p33;
+    e = p12 - 0.5f * p13 + 0.5f * p22 - (11.0f / 12.0f) * p23 + (1.0f / 3.0f) * p33;
+    const kf2 u0p = st.pos + st.vel, u1p = st.vel + st.acc, u2p = st.acc + st.jerk, u3p = st.jerk;
+    // Jd P' Jd^T: C_ij = P_ij + P_i+1,j + P_i,j+1 + P_i+1,j+1 (15 adds)
+    const kf2 c23 = p23 + p33, c22 = (p22 + p23) + c23, c13 = p13 + p23, b12 = p12 + p22, c12 = b12 + c13;
+    const kf2 c11 = (p11 + p12) + b12, c03 = p03 + p13, b02 = p02 + p12, c02 = b02 + c03, b01 = p01 + p11;
+    const kf2 c01 = b01 + b02, c00 = (p00 + p01) + b01;
+    const kf2 y = z - u0p;
+    const kf2 yr = y * krsq2(c00 + c.QpR);  // S before the boost: P00p (with Qp) + R
+    const kf2 bq = kf2{fminf(5.0f, fabsf(yr.x)), fminf(5.0f, fabsf(yr.y))} * c.adapt + 1.0f;  // boost b
+    const kf2 P00p = c00 + bq * c.Qp, P11p = (c11 + e) + bq * c.Q11, P12p = c12 + bq * c.Q12, P13p = c13 + bq * c.Q13;
+    const kf2 P22p = c22 + bq * c.Q22, P23p = c23 + bq * c.Q23, P33p = p33 + bq * c.Q33;
+    const kf2 rs = krsq2(P00p + c.R);
+    kf2 yn = y * rs;
+    yn = kf2{__builtin_amdgcn_fmed3f(yn.x, -c.clip, c.clip), __builtin_amdgcn_fmed3f(yn.y, -c.clip, c.clip)};
+    const kf2 g0 = P00p * rs, g1 = c01 * rs, g2 = c02 * rs, g3 = c03 * rs;
+    st.pos = u0p + g0 * yn;
+    st.vel = u1p + g1 * yn;
+    st.acc = u2p + g2 * yn;
+    st.jerk = u3p + g3 * yn;
+    st.p00 = P00p - g0 * g0;
+    st.p01 = c01 - g1 * g0;
+    st.p02 = c02 - g2 * g0;
+    st.p03 = c03 - g3 * g0;
+    st.p11 = P11p - g1 * g1;
+    st.p12 = P12p - g2 * g1;
+    st.p13 = P13p - g3 * g1;
+    st.p22 = P22p - g2 * g2;
+    st.p23 = P23p - g3 * g2;
+    st.p33 = P33p - g3 * g3;
+    return st.pos;
+}
+
 constexpr int kPk2Warm = 256;
 // can the packed two-segment kernel take windows of n samples with tiles of J steps?
 constexpr bool pk2_fits(int n, int J = 32, int WU = kPk2Warm) { return n >= 4 * WU && ((n + WU) / 2) % J == 0; }
@@ -565,7 +672,11 @@ __device__ __forceinline__ bool kagree(float a, float b, float floor_) {
 // tile's stores every J steps).
 // SCP: cache policy of the detrended rows' stores (16 = sc1: written through to memory, so none are left dirty in
 // the XCDs' L2s for the writeback between the filter and the spectrum launch; 0 = plain)
-template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true, int SCP = 0>
+// NB = 1: the Newton-basis step (kstep_nb2) with its floor guard; a wave whose guard fails re-runs the
+// whole window pair in the original basis (the NB = 0 form) with the floors.  NB = 2 (tools): the
+// guard forced to fail, so every wave takes that re-run.  `fallbacks` (tools): +1 per warm-up
+// re-run, +65536 per guard re-run.
+template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true, int SCP = 0, int NB = 0>
 __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
                                                                 int64_t hop, int64_t n_windows, int n, KP kp,
                                                                 unsigned *fallbacks = nullptr) {
@@ -606,6 +717,9 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     };
     auto tpos = [&](int g) { return (8 * g + rl) * RS + 4 * q; };  // pair index of an IO lane's first sample
 
+    KNb kn;
+    if constexpr (NB) kn = knb_const(kp);
+    kf2 emin = {__builtin_inff(), __builtin_inff()};  // NB: min over the steps of e (floor guard)
     KState2 st;
     kf2 base = {0.f, 0.f};  // each segment's centre: the first sample of its current tile
     KState<float> warm;  // segment B's state after its warm-up
@@ -617,6 +731,9 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
             t[1] = f4v{ra[g].z, rb[g].z, ra[g].w, rb[g].w};
         }
     };
+    // one whole pass over the window pair, in the Newton basis (PNB) or the original one
+    auto pass = [&](auto nb_tag) {
+    constexpr bool PNB = decltype(nb_tag)::value;
     // store_a: segment A's rows are stored (main pass); segment B's always are (ROT: also during its
     // warm-up, into segment A's later region)
     auto run = [&](int c0, int c1, int sA, int sB, auto store_a) {
@@ -633,7 +750,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 __syncthreads();
                 if (c + 1 < c1) issue(c + 1);  // next tile in flight while the lanes filter this one
             }
-            kf2 zrow[J];
+            kf2 zrow[J], eprev;
 #pragma unroll
             for (int j = 0; j < J; j += 2) {
                 const f4v v = *reinterpret_cast<const f4v *>(tile + l * RS + j);
@@ -647,7 +764,9 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
             // excursion instead of the distance from sample 0: a 0.5 level jump inside a window
             // then costs fp32 ~20x less (2-4e-5 -> 1-3e-6 of the spectrum,
             // scripts/kalman_f32_emulation.py).  base - zrow[j] is exact (Sterbenz).
-            if (c == 0) {  // (sample 0, sample L0 - WU): both segments reset at their first sample
+            if (c == 0 && PNB) {
+                knb_reset(st, kp);
+            } else if (c == 0) {  // (sample 0, sample L0 - WU): both segments reset at their first sample
                 KState<float> a;
                 kreset<float>(a, kp, 0.f);
                 st.pos = kf2{0.f, 0.f};
@@ -665,8 +784,20 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                     base = zrow[j];
                 }
                 const kf2 z = zrow[j] - base;  // exact for prices within 2x of the centre (Sterbenz)
-                const kf2 trend = kstep_pk2(st, kc, z);
-                zrow[j] = z - trend;
+                if constexpr (PNB) {
+                    kf2 e;
+                    const kf2 trend = kstep_nb2(st, kn, z, e);
+                    zrow[j] = z - trend;
+                    if (j % 2 == 0) {
+                        eprev = e;
+                    } else {  // one v_min3 per two steps and segment
+                        emin.x = fminf(emin.x, fminf(eprev.x, e.x));
+                        emin.y = fminf(emin.y, fminf(eprev.y, e.y));
+                    }
+                } else {
+                    const kf2 trend = kstep_pk2(st, kc, z);
+                    zrow[j] = z - trend;
+                }
             }
             if (c == WUC - 1) {
                 warm.pos = st.pos.y, warm.vel = st.vel.y, warm.acc = st.acc.y, warm.jerk = st.jerk.y;
@@ -713,6 +844,17 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         st.p23.y = st.p23.x, st.p33.y = st.p33.x;
         base.y = base.x;
         run(WUC, nchunks, nchunks, WUC, std::false_type{});  // only segment B stores
+    }
+    };
+    if constexpr (NB == 0) {
+        pass(std::false_type{});
+    } else {
+        pass(std::true_type{});
+        // the floors were no-ops iff e >= -Qv/2 throughout (kstep_nb2); else the exact original-basis pass
+        if (__ballot(NB == 2 || fminf(emin.x, emin.y) < kn.emin)) {
+            if (fallbacks && l == 0) atomicAdd(fallbacks, 65536u);
+            pass(std::false_type{});
+        }
     }
 }
 

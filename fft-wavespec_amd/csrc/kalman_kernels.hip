@@ -40,20 +40,22 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
 }
 
 // fp32 plans with the reference default flags: two time segments per lane as packed pairs
-// (kalman_pk2_kernel).  Single-wave workgroups: at ~300 VGPRs a SIMD holds one wave of it anyway,
+// (kalman_pk2_kernel), stepped in the Newton basis when the floor guard's premises hold (nb2_ok).  Single-wave workgroups: at ~300 VGPRs a SIMD holds one wave of it anyway,
 // so the dispatcher cannot stack two on one SIMD, and no wave waits at another's barrier
 // (kalman_bench time, C3: 0.55-0.58 ms against 0.60-0.65 ms for 4-wave workgroups, 0.78-0.81 ms
 // for the four-segment lane-pair kernel at two waves per SIMD, 0.69 ms sequential).
 hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
-    // variant 7: the detrended rows written through to memory (A/B, round 5)
-    if (L.variant == 7)
-        hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1, kcore::kPk2Warm, true, 16>), dim3((unsigned)((L.n_windows + 63) / 64)),
-                           dim3(64), 0, stream, static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop,
-                           L.n_windows, L.n, kp, (unsigned *)nullptr);
-    else
-        hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, 1>), dim3((unsigned)((L.n_windows + 63) / 64)), dim3(64), 0, stream,
-                           static_cast<const float *>(L.series), static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp,
-                           (unsigned *)nullptr);
+    const dim3 grid((unsigned)((L.n_windows + 63) / 64));
+    auto args = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, grid, dim3(64), 0, stream, static_cast<const float *>(L.series),
+                           static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp, (unsigned *)nullptr);
+    };
+    if (L.variant == 7)  // the detrended rows written through to memory (A/B, round 5)
+        args(kcore::kalman_pk2_kernel<32, 1, kcore::kPk2Warm, true, 16>);
+    else if (L.variant == 8 || !kcore::nb2_ok(kp))  // the original basis with the reference's floors
+        args(kcore::kalman_pk2_kernel<32, 1>);
+    else  // the Newton basis, floors proven no-ops (guarded; kalman_core.h kstep_nb2)
+        args(kcore::kalman_pk2_kernel<32, 1, kcore::kPk2Warm, true, 0, 1>);
     return hipGetLastError();
 }
 
@@ -66,12 +68,14 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
     __builtin_memcpy(&kp, L.params, sizeof(kp));
     // the reference defaults (adaptive boost + clip, no EMA) run branch-free;
     // other flag sets read them per step.  fp32 default-flag plans of N >= 1024
-    // run two time segments per lane (kalman_pk2_kernel).  L.variant = 1 forces
-    // single-wave workgroups, 2 the sequential fp32 filter (ablations).
+    // run two time segments per lane (kalman_pk2_kernel, Newton basis).  L.variant = 1 forces
+    // single-wave workgroups, 2 the sequential fp32 filter, 8 the two-segment filter in the
+    // original basis (ablations).
     constexpr int kFixed = kcore::kKfAdapt | kcore::kKfClip;
     const bool fixed = kcore::kalman_flags(kp) == kFixed;
     if (L.f32) {
-        if (fixed && (L.variant == 0 || L.variant == 7) && kcore::pk2_fits(L.n)) return launch_pk2(L, kp, stream);
+        if (fixed && (L.variant == 0 || L.variant == 7 || L.variant == 8) && kcore::pk2_fits(L.n))
+            return launch_pk2(L, kp, stream);
         return fixed ? launch_t<float, kFixed>(L, kp, stream) : launch_t<float, kcore::kKfRuntime>(L, kp, stream);
     }
     return fixed ? launch_t<double, kFixed>(L, kp, stream) : launch_t<double, kcore::kKfRuntime>(L, kp, stream);

@@ -5,7 +5,8 @@
 //   kalman_bench time  [reps=10]   variants at C3 (65536 x 4096, f32), back to back
 //                                  and alternating with a 1.5 GB streaming kernel
 //                                  (the C3 step's spectrum launch in between)
-//   kalman_bench check             variants vs a host restatement of the reference step
+//   kalman_bench check [n=256]     variants vs a host restatement of the reference step
+//   kalman_bench ab    [reps=10]   the two-segment filter, original against Newton basis, alternating
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -52,12 +53,12 @@ __global__ __launch_bounds__(256) void stream_copy(const double2 *__restrict__ i
 }
 
 // the packed two-segment kernel (fp32, default flags)
-template <int WAVES, int WU, bool ROT = true>
+template <int WAVES, int WU, bool ROT = true, int NB = 0>
 void launch_pk2(const float *x, float *d, int64_t hop, int64_t W, int n, const kcore::KP &kp, hipStream_t s) {
     const size_t stat = (size_t)WAVES * 64 * 34 * 8;
     const size_t reserve = WAVES == 4 ? 84 * 1024 - stat : 0;
-    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, WAVES, WU, ROT>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)), dim3(64 * WAVES),
-                       reserve, s, x, d, hop, W, n, kp, g_fallbacks);
+    hipLaunchKernelGGL((kcore::kalman_pk2_kernel<32, WAVES, WU, ROT, 0, NB>), dim3((W + 64 * WAVES - 1) / (64 * WAVES)),
+                       dim3(64 * WAVES), reserve, s, x, d, hop, W, n, kp, g_fallbacks);
 }
 
 template <int WU>
@@ -95,6 +96,7 @@ void time_variant(const char *name, const float *x, float *d, const double2 *ci,
     fflush(stdout);
 }
 
+// SEGS = 5: the two-segment kernel in the Newton basis (kstep_nb2)
 template <int WAVES, int WU, int SEGS = 2, bool ROT = true>
 void time_pk2(const char *name, const float *x, float *d, const double2 *ci, double2 *co, int64_t cn, int64_t W, int n, int reps,
               hipStream_t s) {
@@ -107,6 +109,7 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     CK(hipMemset(g_fallbacks, 0, 4));
     auto go = [&]() {
         if constexpr (SEGS == 4) launch_pk4<WU>(x, d, n, W, n, kp, s);
+        else if constexpr (SEGS == 5) launch_pk2<WAVES, WU, ROT, 1>(x, d, n, W, n, kp, s);
         else launch_pk2<WAVES, WU, ROT>(x, d, n, W, n, kp, s);
     };
     go();
@@ -128,8 +131,8 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     }
     unsigned fb = 0;
     CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
-    printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us   fallback waves %u of %lld x %d\n", name,
-           back * 1e3f / reps, alt * 1e3f / reps, fb, (long long)(W / 64), 1 + 2 * reps);
+    printf("%-44s back-to-back %8.1f us   after a streaming kernel %8.1f us   fallback waves %u (+ %u guard) of %lld x %d\n",
+           name, back * 1e3f / reps, alt * 1e3f / reps, fb & 0xffffu, fb >> 16, (long long)(W / 64), 1 + 2 * reps);
     fflush(stdout);
 }
 
@@ -174,7 +177,7 @@ int occ_main(int reps) {
     return 0;
 }
 
-int time_main(int reps) {
+int time_main(int reps, bool nb_only) {
     const int64_t W = 65536;
     const int n = 4096;
     float *x, *d;
@@ -196,6 +199,13 @@ int time_main(int reps) {
     CK(hipMemset(ci, 0, cn * 16));
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    if (nb_only) {  // the round-6 A/B: original basis against the Newton basis, alternating
+        for (int round = 0; round < 4; ++round) {
+            time_pk2<1, 256>("packed 2 segments WU=256, original basis", x, d, ci, co, cn, W, n, reps, s);
+            time_pk2<1, 256, 5>("packed 2 segments WU=256, Newton basis", x, d, ci, co, cn, W, n, reps, s);
+        }
+        return 0;
+    }
     for (int round = 0; round < 2; ++round) {
         printf("round %d\n", round);
         time_variant<kcore::kKfRuntime, true, 1>("1-wave WG, runtime flags, two-stage", x, d, ci, co, cn, W, n, reps, s);
@@ -209,6 +219,7 @@ int time_main(int reps) {
         time_pk2<4, 512>("packed 2 segments WU=512, 4-wave WG", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256, 2, false>("packed 2 segments WU=256, 1-wave WG, unrotated", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256>("packed 2 segments WU=256, 1-wave WG", x, d, ci, co, cn, W, n, reps, s);
+        time_pk2<1, 256, 5>("packed 2 segments WU=256, Newton basis", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 256, 4>("packed 4 segments WU=256, lane pairs", x, d, ci, co, cn, W, n, reps, s);
         time_pk2<1, 512, 4>("packed 4 segments WU=512, lane pairs", x, d, ci, co, cn, W, n, reps, s);
         if (round > 0) continue;
@@ -404,15 +415,28 @@ int check_main(int n) {
             CK(hipMemcpy(dx32, xsf.data(), xsf.size() * 4, hipMemcpyHostToDevice));
             CK(hipMemset(g_fallbacks, 0, 4));
             if (segs == 4) launch_pk4<kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+            else if (segs == 5) launch_pk2<1, kcore::kPk2Warm, true, 1>(dx32, dd32, hop, W, n, kp, 0);
+            else if (segs == 6) launch_pk2<1, kcore::kPk2Warm, true, 2>(dx32, dd32, hop, W, n, kp, 0);
             else if (segs == 3) launch_pk2<4, kcore::kPk2Warm, false>(dx32, dd32, hop, W, n, kp, 0);
             else launch_pk2<1, kcore::kPk2Warm>(dx32, dd32, hop, W, n, kp, 0);
+            unsigned fb = 0;
+            if (segs == 6) {  // the forced guard re-runs in the original basis: bit-identical to that kernel?
+                CK(hipDeviceSynchronize());
+                CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+                launch_pk2<1, kcore::kPk2Warm>(dx32, dq32, hop, W, n, kp, 0);
+                CK(hipDeviceSynchronize());
+                std::vector<float> a(W * n), b(W * n);
+                CK(hipMemcpy(a.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(b.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
+                printf("%-36s bit-identical to the original-basis kernel: %s\n", name,
+                       memcmp(a.data(), b.data(), a.size() * 4) == 0 ? "yes" : "NO");
+            }
             launch<float, 32, 3, true, 4, true>(dx32, dq32, hop, W, n, kp, 0);
             CK(hipDeviceSynchronize());
             std::vector<float> h(W * n), q(W * n);
             CK(hipMemcpy(h.data(), dd32, W * n * 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(q.data(), dq32, W * n * 4, hipMemcpyDeviceToHost));
-            unsigned fb = 0;
-            CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
+            if (segs != 6) CK(hipMemcpy(&fb, g_fallbacks, 4, hipMemcpyDeviceToHost));
             double worst = 0, scale = 0, wseq = 0, wseqv = 0;
             int64_t same = 0;
             for (int64_t i = 0; i < W * n; ++i) {
@@ -422,12 +446,16 @@ int check_main(int n) {
                 wseqv = fmax(wseqv, fabs((double)q[i] - refs[i]));
                 same += h[i] == q[i];
             }
-            printf("%-36s max|d-ref|/max|ref| %.3e (sequential fp32 %.3e)  vs sequential: %.3e, %lld of %lld identical; fallback re-runs %u\n",
-                   name, worst / scale, wseqv / scale, wseq / scale, (long long)same, (long long)(W * n), fb);
+            printf("%-36s max|d-ref|/max|ref| %.3e (sequential fp32 %.3e)  vs sequential: %.3e, %lld of %lld identical; fallback re-runs %u (+ %u guard)\n",
+                   name, worst / scale, wseqv / scale, wseq / scale, (long long)same, (long long)(W * n), fb & 0xffffu, fb >> 16);
         };
         const int L0 = (n + kcore::kPk2Warm) / 2, WU = kcore::kPk2Warm;
         check_pk("f32 packed 2 segments", 2, {});
         check_pk("f32 packed 2 segments, spikes", 2, {L0 - WU});
+        check_pk("f32 packed 2 segments, Newton basis", 5, {});
+        check_pk("f32 packed 2 segments, Newton basis, spikes", 5, {L0 - WU});
+        check_pk("f32 packed 2 segments, Newton basis, guard forced", 6, {});
+        check_pk("f32 packed 2 segments, Newton basis, guard forced, spikes", 6, {L0 - WU});
         check_pk("f32 packed 2 segments unrotated", 3, {});
         check_pk("f32 packed 2 segments unrotated, spikes", 3, {L0 - WU});
         if (kcore::pk4_fits(n)) {
@@ -460,5 +488,6 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&g_dbg, 65536 * 28 * 8));
     if (mode == "check") return check_main(argc > 2 ? atoi(argv[2]) : 256);
     if (mode == "occ") return occ_main(argc > 2 ? atoi(argv[2]) : 10);
-    return time_main(argc > 2 ? atoi(argv[2]) : 10);
+    if (mode == "ab") return time_main(argc > 2 ? atoi(argv[2]) : 10, true);
+    return time_main(argc > 2 ? atoi(argv[2]) : 10, false);
 }

@@ -361,8 +361,10 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    N = 65536 / 131072);
  *  - fp32 Kalman pre-pass (spectrum plans, N <= 16384): 1 = single-wave
  *    workgroups of the one-lane filter, 2 = the sequential one-lane filter,
- *    7 = the packed two-segment filter with its rows written through to memory
- *    (bit-identical to 0);
+ *    7 = the packed two-segment filter in the original basis with its rows
+ *    written through to memory (bit-identical to 8); 8 = the packed two-segment
+ *    filter in the original basis with the reference's diagonal floors (the
+ *    round-5 default; 0 steps in the Newton basis, see kalman_core.h);
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
  *    with the AoS exchange; 3 = 0 with the element loads in natural order

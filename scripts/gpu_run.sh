@@ -19,6 +19,7 @@
 #   sq=<cfg>,<counters>      one rocprofv3 --pmc pass with the given SQ_ counters (<= 8), sq_<cfg>.csv
 #   kbench=<args>            fft-wavespec_amd/bin/kbench <args> (spaces as commas)
 #   kalman=<args>            fft-wavespec_amd/bin/kalman_bench <args>
+#   bin=<name>,<args>        fft-wavespec_amd/bin/<name> <args> (a diagnostic tool, spaces as commas)
 #   harness=<args>           python scripts/<args> (a host-path timing script), spaces as commas
 #   shards[=<args>]          python scripts/emulate_shards.py <tag dir>/shards.json <args> (strong-scaling shards
 #                            emulated one rank at a time on this GPU), args comma-separated
@@ -96,8 +97,18 @@ print('$cfg', '$extra', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step']
         cat $O/kbench.log
         ;;
     kalman)
-        run 300 $O/kalman_bench.log $O/kalman_bench.log fft-wavespec_amd/bin/kalman_bench ${val//,/ }
-        cat $O/kalman_bench.log
+        kl=$O/kalman_bench_${val//,/_}.log
+        run 300 $kl $kl fft-wavespec_amd/bin/kalman_bench ${val//,/ }
+        cat $kl
+        ;;
+    bin)
+        # any diagnostic binary of fft-wavespec_amd/bin: bin=<name>,<args>
+        bn=${val%%,*}
+        ba=""
+        [ "$bn" != "$val" ] && ba=${val#*,}
+        bl=$O/bin_${val//,/_}.log
+        run 300 $bl $bl fft-wavespec_amd/bin/$bn ${ba//,/ }
+        cat $bl
         ;;
     harness)
         hn=${val//,/_}

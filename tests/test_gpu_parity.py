@@ -668,11 +668,12 @@ def _kp(**kw):
     return p
 
 
-@pytest.mark.parametrize("variant", [1, 2, 7])
+@pytest.mark.parametrize("variant", [1, 2, 7, 8])
 def test_kalman_plan_variants(gpu_session, variant):
     """Advisor r05: wsp_plan_set_variant reaches the fp32 Kalman pre-pass of a spectrum plan (it stayed 0 before, so
-    the round-5 "variant 7 neutral" A/B timed one kernel twice).  7 = the packed two-segment filter with its rows
-    written through to memory: bit-identical to the default (0); 1 = single-wave workgroups of the one-lane filter and
+    the round-5 "variant 7 neutral" A/B timed one kernel twice).  8 = the packed two-segment filter in the original
+    basis with the reference's floors (the round-5 default; 0 steps in the Newton basis since round 6); 7 = 8 with its
+    rows written through to memory: bit-identical to 8; 1 = single-wave workgroups of the one-lane filter and
     2 = the sequential one-lane filter: other kernels, held to the fp32 bar against the oracle."""
     torch = pytest.importorskip("torch")
     n, nwin = 2048, 700
@@ -681,7 +682,7 @@ def test_kalman_plan_variants(gpu_session, variant):
     dev = torch.device("cuda", 0)
     d_s = torch.from_numpy(s.astype(np.float32)).to(dev)
     outs = []
-    for v in (0, variant):
+    for v in (0, variant) + ((8,) if variant == 7 else ()):
         plan = bridge.Plan(0, n, n, nwin, "kalman", "hann", precision="f32")
         plan.set_variant(v)
         d_o = torch.full((nwin * (n // 2),), float("nan"), dtype=torch.float32, device=dev)
@@ -689,9 +690,9 @@ def test_kalman_plan_variants(gpu_session, variant):
         torch.cuda.synchronize()
         outs.append(d_o.view(nwin, n // 2).double().cpu().numpy())
         plan.close()
-    base, got = outs
+    base, got = outs[:2]
     if variant == 7:
-        assert np.array_equal(got, base)
+        assert np.array_equal(got, outs[2])
     want = ref(s.astype(np.float32).astype(np.float64), n, n, "kalman", "hann")
     assert oracle.rel_err(got, want) <= TOL["f32"]
     assert oracle.rel_err(base, want) <= TOL["f32"]
@@ -699,9 +700,14 @@ def test_kalman_plan_variants(gpu_session, variant):
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("kw", [dict(ema=20.0), dict(adapt=0.0), dict(clip=0.0), dict(adapt=0.0, clip=0.0, ema=5.0),
-                                dict(follow=2.5, iv=1e-4, ia=-1e-6)])
+                                dict(follow=2.5, iv=1e-4, ia=-1e-6), dict(qp=1e-3, qv=2e-4, qa=5e-5, qj=1e-5),
+                                dict(qj=1e-9), dict(r=0.05), dict(vp=1e-3, vv=50.0, va=0.1, vj=3.0, adapt=2.0, clip=3.0)])
 def test_kalman_params(gpu_session, prec, kw):
-    """gpu_set_kalman_params: non-default flags take the runtime-flag kernel (kalman_kernels.hip)."""
+    """gpu_set_kalman_params: non-default flags take the runtime-flag kernel (kalman_kernels.hip); default flags with
+    other noise levels take the fp32 two-segment filter in the Newton basis when its floor guard's premises hold
+    (slower noise, other initial variances, stronger boost), in the original basis with the floors when they do not
+    (q_jerk at its 1e-9 floor: kalman_core.h nb2_ok).  (The measurement noise at its 1e-9 floor is no test case: the trend
+    then follows every sample and the detrended windows are rounding noise in both filters.)"""
     kp = _kp(**kw)
     n = 1024
     s = synth.random_walk(70 * n, seed=5)
@@ -713,6 +719,27 @@ def test_kalman_params(gpu_session, prec, kw):
     s_ref = s.astype(np.float32).astype(np.float64) if prec == "f32" else s
     r = oracle.batch_spectrum(s_ref, n, n, "kalman", "hann", 0, kalman=kp)
     assert oracle.rel_err(p, r) <= TOL[prec], kw
+
+
+def test_kalman_newton_basis_tool_check(gpu_session):
+    """The Newton-basis filter's own checks (tools/kalman_bench.hip check, N = 4096, hop 37): its result against the
+    fp64 host restatement of StepKalman4D at the fp32 bar with and without forced warm-up re-runs, and with the floor
+    guard forced to fail every wave is bit-identical to the original-basis kernel with the reference's floors."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "fft-wavespec_amd" / "bin" / "kalman_bench"
+    assert exe.exists(), "build() builds bin/kalman_bench"
+    out = subprocess.run([str(exe), "check", "4096"], capture_output=True, text=True, timeout=300, check=True).stdout
+    lines = [ln for ln in out.splitlines() if "Newton basis" in ln]
+    assert len(lines) >= 6, out
+    for ln in lines:
+        if "max|d-ref|/max|ref|" in ln:
+            err = float(ln.split("max|d-ref|/max|ref|")[1].split()[0])
+            assert err <= 1e-5, ln
+    forced = [ln for ln in lines if "bit-identical to the original-basis kernel" in ln]
+    assert len(forced) == 2 and all(ln.rstrip().endswith("yes") for ln in forced), out
+    guard = [ln for ln in lines if "guard forced" in ln and "fallback re-runs" in ln]
+    assert all("+ 2 guard)" in ln for ln in guard), guard  # W = 100 windows: both waves re-ran
 
 
 def test_register_host_records_range(gpu_session):
