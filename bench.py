@@ -620,6 +620,7 @@ def main(argv=None):
         baseline_all = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], budget / 2, cpu_threads())
 
     if rank == 0:
+        valu_bound = bool(wl.valu) and wl.valu["issue_frac"] >= 0.7  # VALU-issue-bound (profiles/valu.json)
         line = {
             "metric": METRIC,
             "value": value,
@@ -636,15 +637,17 @@ def main(argv=None):
             "config": {"workload": wl.describe, "windows_per_gpu": wl.windows, "windows_total": int(total_windows / args.steps),
                        "parallelism": f"windows sharded x{world} ({args.scaling}), no collective",
                        "algorithm": wl.algorithm, **({"c5": wl.layout} if hasattr(wl, "layout") else {})},
-            "roofline": {"bound": "valu" if wl.valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "valu" if valu_bound else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
                          "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a "
                                            "separate run of the same command, scripts/parse_prof.py"
                                            + (f", {next(v for v in TRAFFIC_SOURCE.values() if v)}"
                                               if any(TRAFFIC_SOURCE.values()) else "")
                                            + "), not this run" if wl.traffic else None,
-                         **({"valu": wl.valu, "note": "VALU-issue-bound: achieved / frac are the HBM roofline, "
-                                                      "valu.issue_frac the bound's"} if wl.valu else {}),
+                         **({"valu": wl.valu, "note": ("VALU-issue-bound: achieved / frac are the HBM roofline, "
+                                                       "valu.issue_frac the bound's") if valu_bound else
+                             ("dominant kernel below 0.7 of the VALU issue slots (dependency waits and its own IO): "
+                              "reported against HBM, valu beside it")} if wl.valu else {}),
                          "algorithmic_bytes_per_launch": wl.alg_bytes, "kernel_ms": kernel_s * 1e3,
                          "kernel_ms_max_over_ranks": kernel_s_max * 1e3,
                          "timing": "HIP events on the launch stream around the same K timed steps (rank 0)"},

@@ -674,8 +674,8 @@ __device__ __forceinline__ bool kagree(float a, float b, float floor_) {
 // the XCDs' L2s for the writeback between the filter and the spectrum launch; 0 = plain)
 // NB = 1: the Newton-basis step (kstep_nb2) with its floor guard; a wave whose guard fails re-runs the
 // whole window pair in the original basis (the NB = 0 form) with the floors.  NB = 2 (tools): the
-// guard forced to fail, so every wave takes that re-run.  `fallbacks` (tools): +1 per warm-up
-// re-run, +65536 per guard re-run.
+// guard forced to fail, so every wave takes that re-run; NB = 3 (tools): the tile IO without the
+// filter.  `fallbacks` (tools): +1 per warm-up re-run, +65536 per guard re-run.
 template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true, int SCP = 0, int NB = 0>
 __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
                                                                 int64_t hop, int64_t n_windows, int n, KP kp,
@@ -784,7 +784,9 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                     base = zrow[j];
                 }
                 const kf2 z = zrow[j] - base;  // exact for prices within 2x of the centre (Sterbenz)
-                if constexpr (PNB) {
+                if constexpr (NB == 3) {  // tools: the tile IO alone (no filter)
+                    zrow[j] = z;
+                } else if constexpr (PNB) {
                     kf2 e;
                     const kf2 trend = kstep_nb2(st, kn, z, e);
                     zrow[j] = z - trend;
@@ -828,6 +830,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         }
     };
     run(0, nchunks, 0, WUC, std::true_type{});
+    if constexpr (NB == 3) return;  // tools: IO only, nothing to verify
     // segment A now holds the exact state after sample L0 - 1; segment B held its estimate of it.
     // Both are centred on sample L0 - kRecentre: segment A's last tile is segment B's tile WUC - 1.
     const float fl = 0x1p-24f * (fabsf(base.x) + fabsf(st.pos.x));

@@ -566,7 +566,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
             K.n_windows = c.n_windows;
             K.n = c.n;
             K.f32 = c.f32;
-            K.variant = c.variant;  // the plan's Kalman pre-pass forms (wsp_plan_set_variant: 1, 2, 7)
+            K.variant = c.variant;  // the plan's Kalman pre-pass forms (wsp_plan_set_variant: 1, 2, 7, 8)
             memcpy(K.params, kalman, sizeof(K.params));
             HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
             G.series = wsb + ws.det;
@@ -637,6 +637,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         K.n_windows = c.n_windows;
         K.n = c.n;
         K.f32 = c.f32;
+        K.variant = c.variant;  // the plan's Kalman pre-pass forms (wsp_plan_set_variant: 1, 2, 7, 8)
         memcpy(K.params, kalman, sizeof(K.params));
         HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
         L.series = d_ws;

@@ -110,6 +110,7 @@ void time_pk2(const char *name, const float *x, float *d, const double2 *ci, dou
     auto go = [&]() {
         if constexpr (SEGS == 4) launch_pk4<WU>(x, d, n, W, n, kp, s);
         else if constexpr (SEGS == 5) launch_pk2<WAVES, WU, ROT, 1>(x, d, n, W, n, kp, s);
+        else if constexpr (SEGS == 6) launch_pk2<WAVES, WU, ROT, 3>(x, d, n, W, n, kp, s);
         else launch_pk2<WAVES, WU, ROT>(x, d, n, W, n, kp, s);
     };
     go();
@@ -203,6 +204,7 @@ int time_main(int reps, bool nb_only) {
         for (int round = 0; round < 4; ++round) {
             time_pk2<1, 256>("packed 2 segments WU=256, original basis", x, d, ci, co, cn, W, n, reps, s);
             time_pk2<1, 256, 5>("packed 2 segments WU=256, Newton basis", x, d, ci, co, cn, W, n, reps, s);
+            time_pk2<1, 256, 6>("packed 2 segments WU=256, tile IO only", x, d, ci, co, cn, W, n, reps, s);
         }
         return 0;
     }

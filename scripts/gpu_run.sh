@@ -17,6 +17,7 @@
 #                            rocprofv3 kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own
 #                            passes (scripts/gpu_profile.sh), parsed by scripts/parse_prof.py
 #   sq=<cfg>,<counters>      one rocprofv3 --pmc pass with the given SQ_ counters (<= 8), sq_<cfg>.csv
+#   sqv=<cfg>,<v>,<counters> the same on plan variant <v> (bench.py --variant), sq_<cfg>_v<v>
 #   kbench=<args>            fft-wavespec_amd/bin/kbench <args> (spaces as commas)
 #   kalman=<args>            fft-wavespec_amd/bin/kalman_bench <args>
 #   bin=<name>,<args>        fft-wavespec_amd/bin/<name> <args> (a diagnostic tool, spaces as commas)
@@ -91,6 +92,15 @@ print('$cfg', '$extra', d['config'].get('algorithm'), '%.4f ms'%d['ms_per_step']
         ctr=${val#*,}
         run 120 $O/sq_$cfg.log $O/sq_$cfg.log rocprofv3 --pmc ${ctr//,/ } --kernel-trace --output-format csv -d $O/sq_$cfg -o run -- \
             python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline
+        ;;
+    sqv)
+        # sqv=<cfg>,<plan variant>,<counters>: the same pass on a plan variant, sq_<cfg>_v<variant>
+        cfg=${val%%,*}
+        rest=${val#*,}
+        var=${rest%%,*}
+        ctr=${rest#*,}
+        run 120 $O/sq_${cfg}_v$var.log $O/sq_${cfg}_v$var.log rocprofv3 --pmc ${ctr//,/ } --kernel-trace --output-format csv \
+            -d $O/sq_${cfg}_v$var -o run -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --variant $var
         ;;
     kbench)
         run 300 $O/kbench.log $O/kbench.log fft-wavespec_amd/bin/kbench ${val//,/ }
