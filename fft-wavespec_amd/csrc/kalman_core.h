@@ -706,6 +706,13 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, (int)voff, (int)soff, SCP);
     };
+    // segment B's warm-up rows (ROT stores them so that every tile issues the same stores, see above): through an
+    // empty descriptor, which drops them -- the same vmcnt bookkeeping without their 6 % of the written bytes
+    const auto rnull = kbuf(dout, 0u);
+    auto st4_warm = [&](f4v v, uint32_t voff, uint32_t soff, bool drop) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), drop ? rnull : rout, (int)voff, (int)soff, SCP);
+    };
     f4v ra[8], rb[8];
     auto issue = [&](int c) {
         const uint32_t vc = vin + (uint32_t)(c * J * (int)sizeof(float));
@@ -817,7 +824,7 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 const f4v *t = reinterpret_cast<const f4v *>(tile + tpos(g));
                 const f4v u = t[0], v = t[1];
                 if (ROT ? SA : c >= sA) st4(f4v{u.x, u.z, v.x, v.z}, vc, out_off(g, 0));
-                if (ROT || c >= sB) st4(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1));
+                if (ROT || c >= sB) st4_warm(f4v{u.y, u.w, v.y, v.w}, vc, out_off(g, 1), c < sB);
             }
             __syncthreads();
             if constexpr (ROT) {
