@@ -90,6 +90,11 @@ def parse(argv=None):
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: run exactly rank R's part of the --scaling strong split over G ranks on this one GPU "
                          "(single-GPU emulation of one rank of a G-GPU run, not a scaling measurement)")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                    help="roofline.traffic from this run: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over a 3-step run "
+                         "of the same command, as child processes after the timed region (scripts/pmc_traffic.py); "
+                         "auto = on for a one-GPU line with its CPU baseline (the driver's default line and the "
+                         "closing check), off for A/B and shard runs, which keep the committed profiles/traffic.json")
     ap.add_argument("--plan-only", action="store_true",
                     help="print every rank's shard of the batch and exit, without touching a GPU (CPU tests)")
     return ap.parse_args(argv)
@@ -559,6 +564,35 @@ class C5Batch(Workload):
             j[0].close()
 
 
+def want_pmc(args) -> bool:
+    """--pmc auto: this run's traffic for a one-GPU line that carries its CPU baseline (the driver's default line,
+    the closing check's lines), never inside a PMC child or for an emulated shard."""
+    if os.environ.get("WSP_BENCH_PMC_CHILD") or args.emulate_shard:
+        return False
+    return args.pmc == "on" or (args.pmc == "auto" and not args.no_cpu_baseline)
+
+
+def run_pmc(args, argv):
+    """rocprofv3 FETCH_SIZE and WRITE_SIZE passes (each its own child run, scripts/pmc_traffic.py) over 3 steps of
+    this same command; the per-step bytes, or None (no rocprofv3, a failed or timed-out pass)."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import pmc_traffic
+    drop = {"--steps": 1, "--warmup": 1, "--pmc": 1, "--cpu-seconds": 1, "--no-cpu-baseline": 0, "--no-settle": 0}
+    rest, i = [], 0
+    while i < len(argv):
+        a = argv[i]
+        name = a.split("=", 1)[0]
+        if name in drop:
+            i += 1 + (drop[name] if "=" not in a else 0)
+            continue
+        rest.append(a)
+        i += 1
+    cmd = [sys.executable, str(Path(__file__).resolve())] + rest + ["--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                                                                    "--no-settle", "--pmc", "off"]
+    key = pmc_traffic.bench_key(args.config, args.algo, args.variant, args.c5_mode)
+    return pmc_traffic.collect(cmd, args.config, key)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -619,6 +653,20 @@ def main(argv=None):
         baseline = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], budget)
         baseline_all = cpu_baseline(wl.cpu_cfg[0], wl.cpu_cfg[1], budget / 2, cpu_threads())
 
+    pmc = None
+    if rank == 0 and world == 1 and want_pmc(args):
+        pmc = run_pmc(args, argv)
+    if pmc:
+        traffic, traffic_source = pmc["hbm_bytes_per_launch"], (
+            "this run: " + pmc["method"] + " -- child processes of this bench.py after its timed region, over 3 steps "
+            "of the same command (scripts/pmc_traffic.py)")
+    else:
+        traffic = wl.traffic
+        traffic_source = ("profiles/traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a separate run of the same "
+                          "command, scripts/parse_prof.py"
+                          + (f", {next(v for v in TRAFFIC_SOURCE.values() if v)}" if any(TRAFFIC_SOURCE.values()) else "")
+                          + "), not this run") if wl.traffic else None
+
     if rank == 0:
         valu_bound = bool(wl.valu) and wl.valu["issue_frac"] >= 0.7  # VALU-issue-bound (profiles/valu.json)
         line = {
@@ -638,12 +686,9 @@ def main(argv=None):
                        "parallelism": f"windows sharded x{world} ({args.scaling}), no collective",
                        "algorithm": wl.algorithm, **({"c5": wl.layout} if hasattr(wl, "layout") else {})},
             "roofline": {"bound": "valu" if valu_bound else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": wl.traffic,
-                         "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a "
-                                           "separate run of the same command, scripts/parse_prof.py"
-                                           + (f", {next(v for v in TRAFFIC_SOURCE.values() if v)}"
-                                              if any(TRAFFIC_SOURCE.values()) else "")
-                                           + "), not this run" if wl.traffic else None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_source,
+                         **({"traffic_read_bytes": pmc["read_bytes_corrected"], "traffic_write_bytes": pmc["write_bytes"]}
+                            if pmc else {}),
                          **({"valu": wl.valu, "note": ("VALU-issue-bound: achieved / frac are the HBM roofline, "
                                                        "valu.issue_frac the bound's") if valu_bound else
                              ("dominant kernel below 0.7 of the VALU issue slots (dependency waits and its own IO): "
