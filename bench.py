@@ -372,6 +372,8 @@ class SingleBatch(Workload):
         from wavespec_amd import bridge, synth
         cfg = dict(synth.CONFIGS[name])
         cfg.setdefault("trend_period", 0)
+        if os.environ.get("WSP_BENCH_WINDOW"):  # ablation only: another window on the same batch (not a BASELINE config)
+            cfg["window"] = os.environ["WSP_BENCH_WINDOW"]
         dev = torch.device("cuda", local_rank)
         n, hop, w = cfg["n"], cfg["hop"], cfg["windows"]
         f32 = cfg["precision"] == "f32"

@@ -677,12 +677,16 @@ __device__ __forceinline__ bool kagree(float a, float b, float floor_) {
 // guard forced to fail, so every wave takes that re-run; NB = 3 (tools): the tile IO without the
 // filter.  `fallbacks` (tools): +1 per warm-up re-run, +65536 per guard re-run.
 template <int J, int WAVES, int WU = kPk2Warm, bool ROT = true, int SCP = 0, int NB = 0>
+// wpairs (optional): the window as (h_j, h_(j + seg_off)) pairs, j < L0, staged once into dynamic LDS (L0 x 8 B) and
+// multiplied into both segments' detrended rows on their way out (the spectrum launch then takes no window).
 __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__restrict__ series, float *__restrict__ dout,
                                                                 int64_t hop, int64_t n_windows, int n, KP kp,
-                                                                unsigned *fallbacks = nullptr) {
+                                                                unsigned *fallbacks = nullptr,
+                                                                const float *__restrict__ wpairs = nullptr) {
     static_assert(J == 32 && WU % J == 0, "8 lanes x 4 samples per row, whole tiles of warm-up");
     constexpr int RS = J + 2;  // row stride in pairs
     __shared__ __attribute__((aligned(16))) kf2 tiles[WAVES][64 * RS];
+    extern __shared__ __attribute__((aligned(16))) kf2 wlds[];  // window pairs (wpairs != nullptr)
     typedef float f4v __attribute__((ext_vector_type(4)));
     const int l = threadIdx.x % 64, wv = WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / 64) : 0;
     kf2 *tile = tiles[wv];
@@ -724,6 +728,11 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
     };
     auto tpos = [&](int g) { return (8 * g + rl) * RS + 4 * q; };  // pair index of an IO lane's first sample
 
+    const bool win = wpairs != nullptr;
+    if (win) {  // the window pairs into LDS, once per workgroup
+        for (int i = threadIdx.x; i < L0; i += 64 * WAVES) wlds[i] = reinterpret_cast<const kf2 *>(wpairs)[i];
+        __syncthreads();
+    }
     KNb kn;
     if constexpr (NB) kn = knb_const(kp);
     kf2 emin = {__builtin_inff(), __builtin_inff()};  // NB: min over the steps of e (floor guard)
@@ -813,6 +822,14 @@ __global__ __launch_bounds__(64 * WAVES) void kalman_pk2_kernel(const float *__r
                 warm.p00 = st.p00.y, warm.p01 = st.p01.y, warm.p02 = st.p02.y, warm.p03 = st.p03.y;
                 warm.p11 = st.p11.y, warm.p12 = st.p12.y, warm.p13 = st.p13.y, warm.p22 = st.p22.y;
                 warm.p23 = st.p23.y, warm.p33 = st.p33.y;
+            }
+            if (win) {  // window values of samples c J + j (segment A) and seg_off + c J + j (B): broadcast LDS reads
+#pragma unroll
+                for (int j = 0; j < J; j += 2) {
+                    const f4v h = *reinterpret_cast<const f4v *>(wlds + c * J + j);
+                    zrow[j] *= kf2{h.x, h.y};
+                    zrow[j + 1] *= kf2{h.z, h.w};
+                }
             }
 #pragma unroll
             for (int j = 0; j < J; j += 2)

@@ -44,11 +44,18 @@ template <typename T, int FL> hipError_t launch_t(const KalmanLaunch &L, const K
 // so the dispatcher cannot stack two on one SIMD, and no wave waits at another's barrier
 // (kalman_bench time, C3: 0.55-0.58 ms against 0.60-0.65 ms for 4-wave workgroups, 0.78-0.81 ms
 // for the four-segment lane-pair kernel at two waves per SIMD, 0.69 ms sequential).
+constexpr int kFoldMaxPairs = 2176;  // window pairs in LDS: N <= 4096 (17 KiB beside the 17 KiB tile, 4 waves per CU)
+
 hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
     const dim3 grid((unsigned)((L.n_windows + 63) / 64));
+    const bool fold = kalman_folds_window(L);
+    int l0 = 0, seg_off = 0;
+    kalman_pair_geometry(L.n, &l0, &seg_off);
+    const size_t lds = fold ? (size_t)l0 * 2 * sizeof(float) : 0;
     auto args = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, grid, dim3(64), 0, stream, static_cast<const float *>(L.series),
-                           static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp, (unsigned *)nullptr);
+        hipLaunchKernelGGL(kernel, grid, dim3(64), lds, stream, static_cast<const float *>(L.series),
+                           static_cast<float *>(L.detrended), L.hop, L.n_windows, L.n, kp, (unsigned *)nullptr,
+                           fold ? L.window_pairs : (const float *)nullptr);
     };
     if (L.variant == 7)  // the detrended rows written through to memory (A/B, round 5)
         args(kcore::kalman_pk2_kernel<32, 1, kcore::kPk2Warm, true, 16>);
@@ -59,7 +66,27 @@ hipError_t launch_pk2(const KalmanLaunch &L, const KP &kp, hipStream_t stream) {
     return hipGetLastError();
 }
 
+bool pk2_path(const KalmanLaunch &L, const KP &kp) {
+    constexpr int kFixed = kcore::kKfAdapt | kcore::kKfClip;
+    return L.f32 && kcore::kalman_flags(kp) == kFixed && (L.variant == 0 || L.variant == 7 || L.variant == 8 || L.variant == 9) &&
+           kcore::pk2_fits(L.n);
+}
+
 }  // namespace
+
+void kalman_pair_geometry(int n, int *l0, int *seg_off) {
+    *l0 = (n + kcore::kPk2Warm) / 2;
+    *seg_off = *l0 - kcore::kPk2Warm;
+}
+
+bool kalman_folds_window(const KalmanLaunch &L) {
+    if (!L.window_pairs || L.n_windows <= 0) return false;
+    KP kp;
+    __builtin_memcpy(&kp, L.params, sizeof(kp));
+    int l0 = 0, seg_off = 0;
+    kalman_pair_geometry(L.n, &l0, &seg_off);
+    return pk2_path(L, kp) && l0 <= kFoldMaxPairs;
+}
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
     if (L.n_windows <= 0) return hipSuccess;
@@ -74,8 +101,7 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream) {
     constexpr int kFixed = kcore::kKfAdapt | kcore::kKfClip;
     const bool fixed = kcore::kalman_flags(kp) == kFixed;
     if (L.f32) {
-        if (fixed && (L.variant == 0 || L.variant == 7 || L.variant == 8) && kcore::pk2_fits(L.n))
-            return launch_pk2(L, kp, stream);
+        if (pk2_path(L, kp)) return launch_pk2(L, kp, stream);
         return fixed ? launch_t<float, kFixed>(L, kp, stream) : launch_t<float, kcore::kKfRuntime>(L, kp, stream);
     }
     return fixed ? launch_t<double, kFixed>(L, kp, stream) : launch_t<double, kcore::kKfRuntime>(L, kp, stream);

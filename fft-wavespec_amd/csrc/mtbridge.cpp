@@ -216,6 +216,49 @@ int get_tables(int dev, int log2n, bool f32, Tables *out) {
     return MTB_OK;
 }
 
+// Window pairs of the fp32 two-segment Kalman filter per (device, N, window) (kalman_folds_window): float pairs
+// {h(j), h(j + seg_off)}, j < L0, of the reference's symmetric windows (L/WaveSpecZZ_1.0.2.mq5:884-914, denominator
+// N - 1), each value from long double rounded once.
+std::mutex g_wpairs_mu;
+std::map<std::tuple<int, int, int>, void *> *g_wpairs = new std::map<std::tuple<int, int, int>, void *>();
+
+long double window_value_ld(int window, int i, int n) {
+    const long double pi = 3.141592653589793238462643383279502884L, th = 2.0L * pi * (long double)i / (long double)(n - 1);
+    switch (window) {
+    case MTB_WINDOW_HANN: return 0.5L * (1.0L - cosl(th));
+    case MTB_WINDOW_HAMMING: return 0.54L - 0.46L * cosl(th);
+    case MTB_WINDOW_BLACKMAN: return 0.42L - 0.5L * cosl(th) + 0.08L * cosl(2.0L * th);
+    case MTB_WINDOW_BARTLETT: return 1.0L - fabsl((2.0L * (long double)i - (long double)n + 1.0L) / (long double)(n - 1));
+    default: return 1.0L;
+    }
+}
+
+int get_window_pairs(int dev, int n, int window, const float **out) {
+    *out = nullptr;
+    if (window == MTB_WINDOW_NONE) return MTB_OK;
+    std::lock_guard<std::mutex> lk(g_wpairs_mu);
+    auto key = std::make_tuple(dev, n, window);
+    auto it = g_wpairs->find(key);
+    if (it != g_wpairs->end()) {
+        *out = static_cast<const float *>(it->second);
+        return MTB_OK;
+    }
+    int l0 = 0, seg_off = 0;
+    kalman_pair_geometry(n, &l0, &seg_off);
+    std::vector<float> h((size_t)l0 * 2);
+    for (int j = 0; j < l0; ++j) {
+        h[2 * j] = (float)window_value_ld(window, j, n);
+        h[2 * j + 1] = j + seg_off < n ? (float)window_value_ld(window, j + seg_off, n) : 0.0f;
+    }
+    void *d = nullptr;
+    HIP_OR(hipSetDevice(dev), MTB_BACKEND_UNAVAILABLE);
+    HIP_OR(hipMalloc(&d, h.size() * sizeof(float)), MTB_NO_MEM);
+    HIP_OR(hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice), MTB_INTERNAL_ERROR);
+    (*g_wpairs)[key] = d;
+    *out = static_cast<const float *>(d);
+    return MTB_OK;
+}
+
 // Sliding-DFT tables per (device, N, window) (sliding_dft.hip), double complex, long double
 // arithmetic rounded once: [nf][N/2] omega_f(k) = e^{2 pi j (k/N + m_f/(N-1))}, m_f = 0, +1, -1, +2, -2;
 // [N/2] H_k = DFT_k of the window; [(nf-1)/2][N] e^{-j m th i}, th = 2 pi/(N-1).
@@ -625,6 +668,7 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         return MTB_OK;
     }
     SpectrumLaunch L{};
+    bool window_folded = false;  // the Kalman pre-pass applied the window (kalman_folds_window)
     L.grid = c.grid;
     L.series = d_series;
     L.hop = c.hop;
@@ -639,13 +683,20 @@ int enqueue(int dev, const Config &c, const double *kalman, const void *d_series
         K.f32 = c.f32;
         K.variant = c.variant;  // the plan's Kalman pre-pass forms (wsp_plan_set_variant: 1, 2, 7, 8)
         memcpy(K.params, kalman, sizeof(K.params));
+        // the fp32 two-segment filter multiplies the window into its rows (round 6): one multiply per sample in a
+        // filter bound by its IO instead of the window recurrence in the VALU-bound fp32 spectrum pass
+        if (c.f32 && c.variant != 9) {
+            st = get_window_pairs(dev, c.n, c.window, &K.window_pairs);
+            if (st != MTB_OK) return st;
+        }
         HIP_OR(launch_kalman_detrend(K, s), MTB_INTERNAL_ERROR);
+        if (kalman_folds_window(K)) window_folded = true;
         L.series = d_ws;
         L.hop = c.n;
         L.detrend = kDetrendNone;
     }
     L.out = d_out;
-    L.window = c.window;
+    L.window = window_folded ? MTB_WINDOW_NONE : c.window;
     L.twiddle = t.tw;
     L.n_windows = c.n_windows;
     L.log2n = c.log2n;
@@ -2056,9 +2107,9 @@ MTB_API int32_t wsp_plan_set_algorithm(int64_t plan, int32_t algo) {
 
 MTB_API int32_t wsp_plan_set_variant(int64_t plan, int32_t variant) {
     std::shared_ptr<Plan> p = find_plan(plan);
-    constexpr int kMaxVariant = 8;  // kernel forms of the ablations (wsp_internal.h)
+    constexpr int kMaxVariant = 9;  // kernel forms of the ablations (wsp_internal.h)
     if (!p || variant < 0 || variant > kMaxVariant) {
-        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..8", (long long)plan, variant);
+        set_error("wsp_plan_set_variant(%lld, %d): unknown plan or variant outside 0..9", (long long)plan, variant);
         return MTB_BAD_ARGS;
     }
     std::lock_guard<std::mutex> lk(p->mu);

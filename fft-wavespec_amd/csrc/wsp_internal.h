@@ -107,9 +107,18 @@ struct KalmanLaunch {
     bool f32;
     double params[16];    // L/WaveSpecZZ_1.0.3-pla-kalman-fast.mq5:886-901 order
     int variant;          // 0 auto, 1 = single-wave workgroups only, 2 = sequential fp32 filter (ablations)
+    // fp32 two-segment filter only (kalman_folds_window): the window, as (h_j, h_(j + seg_off)) float pairs for
+    // j < L0 (kalman_window_pairs), multiplied into the detrended rows it writes; the spectrum launch then runs
+    // with no window.  nullptr = rows leave unwindowed.
+    const float *window_pairs;
 };
 
 hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t stream);
+// does launch_kalman_detrend multiply the window into the rows of this launch (n <= 4096, the fp32 two-segment
+// filter, a window table given)?  Then the spectrum kernel after it must run with no window.
+bool kalman_folds_window(const KalmanLaunch &L);
+// window pairs of the two-segment filter for window length n: {L0 = (n + WU) / 2, seg_off = L0 - WU}
+void kalman_pair_geometry(int n, int *l0, int *seg_off);
 
 // hop = 1 batches by a seeded sliding DFT (sliding_dft.hip): N = 512 .. 8192, detrend none or
 // mean, windows none / Hann / Hamming / Blackman (sums of nf = 1, 3, 5 complex exponentials),

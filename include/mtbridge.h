@@ -364,7 +364,9 @@ MTB_API int32_t wsp_plan_set_trace(int64_t plan, void *d_trace, int64_t capacity
  *    7 = the packed two-segment filter in the original basis with its rows
  *    written through to memory (bit-identical to 8); 8 = the packed two-segment
  *    filter in the original basis with the reference's diagonal floors (the
- *    round-5 default; 0 steps in the Newton basis, see kalman_core.h);
+ *    round-5 default; 0 steps in the Newton basis, see kalman_core.h); 9 = the
+ *    default filter with the window applied by the spectrum kernel (0 has
+ *    the two-segment filter multiply it into its rows at N <= 4096);
  *  - inverse plans (wsp_plan_create_inverse, N = 2048 .. 8192): 1 = the
  *    C2R pre-step through LDS (round-1 form), 2 = the pre-step in registers
  *    with the AoS exchange; 3 = 0 with the element loads in natural order

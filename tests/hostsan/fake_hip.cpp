@@ -426,6 +426,13 @@ hipError_t launch_kalman_detrend(const KalmanLaunch &L, hipStream_t s) {  // det
     });
     return hipSuccess;
 }
+// the real filter folds the window into its rows at N <= 4096 (kalman_kernels.hip); the fake never does, so the
+// fake spectrum launch sees the plan's window as before
+bool kalman_folds_window(const KalmanLaunch &) { return false; }
+void kalman_pair_geometry(int n, int *l0, int *seg_off) {
+    *l0 = (n + 256) / 2;
+    *seg_off = *l0 - 256;
+}
 hipError_t launch_inverse(const InverseLaunch &L, hipStream_t s) {
     check_op(s, {L.in, L.out}, L.n_windows);
     const InverseLaunch c = L;

@@ -724,6 +724,33 @@ def test_kalman_params(gpu_session, prec, kw):
     assert oracle.rel_err(p, r) <= TOL[prec], kw
 
 
+@pytest.mark.parametrize("window", ["hann", "hamming", "blackman", "bartlett", "none"])
+@pytest.mark.parametrize("n,nwin,hop", [(1024, 130, 1024), (4096, 70, 4096), (4096, 65, 37), (8192, 9, 8192)])
+def test_kalman_window_fold(gpu_session, window, n, nwin, hop):
+    """The fp32 two-segment Kalman filter multiplies the plan's window into its rows at N <= 4096 (window pairs staged
+    in LDS) and the spectrum launch then takes none; variant 9 keeps the window in the spectrum kernel, and N = 8192
+    never folds.  Both against the oracle at the fp32 bar for every window, ragged tiles and overlapping windows
+    included, and against each other."""
+    torch = pytest.importorskip("torch")
+    s = synth.random_walk((nwin - 1) * hop + n, seed=n + nwin + hop)
+    dev = torch.device("cuda", 0)
+    d_s = torch.from_numpy(s.astype(np.float32)).to(dev)
+    outs = []
+    for v in (0, 9):
+        plan = bridge.Plan(0, n, hop, nwin, "kalman", window, precision="f32")
+        plan.set_variant(v)
+        d_o = torch.full((nwin * (n // 2),), float("nan"), dtype=torch.float32, device=dev)
+        plan.execute(d_s.data_ptr(), d_o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(d_o.view(nwin, n // 2).double().cpu().numpy())
+        plan.close()
+    want = ref(s.astype(np.float32).astype(np.float64), n, hop, "kalman", window)
+    for got in outs:
+        assert oracle.rel_err(got, want) <= TOL["f32"], window
+        assert oracle.inband_err(got, want, *oracle.band(n)) <= TOL["f32"], window
+    assert oracle.rel_err(outs[0], outs[1]) <= 2e-6
+
+
 def test_kalman_newton_basis_tool_check(gpu_session):
     """The Newton-basis filter's own checks (tools/kalman_bench.hip check, N = 4096, hop 37): its result against the
     fp64 host restatement of StepKalman4D at the fp32 bar with and without forced warm-up re-runs, and with the floor
