@@ -93,6 +93,9 @@ def _pass(counter: str, cmd: list, workdir: str, timeout: float) -> list | None:
     out = os.path.join(workdir, counter.lower())
     full = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "run", "--"] + cmd
     env = dict(os.environ, WSP_BENCH_PMC_CHILD="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+              "MASTER_PORT"):  # a torchrun parent's rendezvous is not the child's: it runs as a lone rank
+        env.pop(k, None)
     try:
         p = subprocess.Popen(full, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env, start_new_session=True)
     except OSError:

@@ -331,6 +331,18 @@ def test_topk_f32_and_plan(gpu_session):
     plan.close()
 
 
+@pytest.mark.parametrize("window", ["hann", "blackman"])
+def test_topk_f32_kalman_window_fold(gpu_session, window):
+    """fp32 Kalman top-k records: the filter folds the window into its rows (kalman_folds_window) and the top-k launch
+    runs unwindowed -- bins, powers and Re/Im of the winners as the oracle's windowed spectrum at the fp32 bar."""
+    n, w = 2048, 200
+    s = synth.random_walk(n * w, seed=29)
+    s32 = s.astype(np.float32).astype(np.float64)
+    got = bridge.spectrum_topk_batch(s32, n, n, "kalman", window, 0, "f32", 8, 18, 200)
+    want = oracle.batch_topk(s32, n, n, "kalman", window, 0, None, 8, 18, 200)
+    _topk_match(got, want, 1e-5, ref(s32, n, n, "kalman", window).max(axis=1))
+
+
 # ---------------------------------------------------------------- SURVEY 8f row 2: inverse + phase
 def _nyquist_free(x):
     n = x.shape[-1]
