@@ -1205,7 +1205,6 @@ struct Plan {
     std::shared_ptr<void> ws;
     size_t ws_bytes = 0;
     hipEvent_t done = nullptr;       // the last workspace execute's completion
-    hipStream_t done_stream = nullptr;
     bool done_recorded = false;
     ~Plan() {
         if (done) (void)hipEventDestroy(done);
@@ -2047,12 +2046,12 @@ MTB_API int32_t wsp_plan_execute(int64_t plan, const void *d_series, void *d_out
                     return MTB_INTERNAL_ERROR;
                 }
             }
-            if (p->done_recorded && p->done_stream != stream) HIP_OR(hipStreamWaitEvent(stream, p->done, 0), MTB_INTERNAL_ERROR);
+            // always (as for the counter slots): a destroyed stream's handle can come back as a new stream's
+            if (p->done_recorded) HIP_OR(hipStreamWaitEvent(stream, p->done, 0), MTB_INTERNAL_ERROR);
             const int st = enqueue(p->dev, c, p->kalman, d_series, d_out, ws.get(), stream);
             if (st != MTB_OK) return st;
             HIP_OR(hipEventRecord(p->done, stream), MTB_INTERNAL_ERROR);
             p->done_recorded = true;
-            p->done_stream = stream;
             return MTB_OK;
         }
     }
