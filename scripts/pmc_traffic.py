@@ -115,7 +115,7 @@ def _pass(counter: str, cmd: list, workdir: str, timeout: float) -> list | None:
     return r or None
 
 
-def collect(cmd: list, cfg: str, key: str, timeout: float = 180.0) -> dict | None:
+def collect(cmd: list, cfg: str, key: str, timeout: float = 120.0) -> dict | None:
     """FETCH_SIZE and WRITE_SIZE passes over `cmd` (a short bench.py run of the same configuration), each in
     its own rocprofv3 run; the summarize() dict, or None when rocprofv3 is missing or a pass fails."""
     if shutil.which("rocprofv3") is None:

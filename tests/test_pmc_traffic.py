@@ -44,7 +44,7 @@ def test_run_pmc_child_command(monkeypatch):
     """The child runs the same configuration for 3 steps without the CPU baseline, settle or PMC of its own."""
     seen = {}
 
-    def fake(cmd, cfg, key, timeout=180.0):
+    def fake(cmd, cfg, key, timeout=120.0):
         seen.update(cmd=cmd, cfg=cfg, key=key)
         return {"hbm_bytes_per_launch": 1.0}
 
