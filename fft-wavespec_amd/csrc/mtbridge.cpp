@@ -1404,12 +1404,16 @@ int group_execute_mixed(Group &g, const void *const *d_series, void *const *d_ou
     // for the single-length ranks).  Measured and dropped (r05n): one task per CU at segments just covering the CUs
     // (S = 110 instead of 128 on a 2048-point shard) -- every rank 4-10 % slower: the shard's slide is bound by the
     // aggregate write rate, not by idle CUs, and the extra seeds cost more.
+    // Round 6: such a batch takes 64-window segments instead of the floor's 128 -- several rounds of shorter tasks, so
+    // that a CU whose tasks end early takes more instead of idling while its slowest one slides alone (the single-
+    // length slide's finding, sliding_core.h launch_t): 1/8 C5 shards' worst rank 0.1172 -> 0.1115 ms with 64-window
+    // segments on one box (r06c5, each rank the median of 3 passes), the whole batch (above the floor) unchanged.
     bool small = false;
     if (policy) {
         S = (int64_t)std::ceil((double)bins / (2.0 * res * 2048.0));
         above_floor = S > 128;
         small = !above_floor && (g.mode == 0 || g.mode == 6);
-        S = std::min<int64_t>(256, std::max<int64_t>(128, S));
+        S = above_floor ? std::min<int64_t>(256, S) : (g.mode == 0 || g.mode == 6 ? 64 : 128);
     }
     // Half-length segments for the last class (the shortest windows, picked up last, drain the launch) when the
     // batch is large enough that the policy's segments are above the floor: the full C5 batch 0.7322-0.7325 ms
